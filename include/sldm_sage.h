@@ -1,0 +1,115 @@
+/*
+ * sldm_sage.h — C ABI of the MI355X-native SageBlock hot path (libsldm_sage.so).
+ *
+ * The reference path is pure Python over PyTorch + torch_geometric 2.7.0 and has
+ * no FFI of its own (no native code in the reference).  Each entry
+ * point below replaces one step of what the reference executes per
+ * SageBlock.forward (/root/reference/src/models/blocks/sageblock.py:16-20) and
+ * its autograd backward; the replaced step is cited on each declaration.
+ *
+ * Conventions
+ *   - every pointer is a DEVICE pointer unless stated; the library allocates
+ *     nothing: callers pass outputs and workspaces (the Python host code uses
+ *     the PyTorch caching allocator);
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream); all
+ *     work is enqueued asynchronously on it; no entry point synchronises;
+ *   - matrices are row-major with a leading dimension in ELEMENTS;
+ *   - dtype codes: SLDM_F32 (fp32) and SLDM_BF16 (bf16 storage, fp32 math);
+ *   - return value: SLDM_OK or an error code; sldm_last_error() then returns a
+ *     thread-local message.  Launch failures are reported from hipGetLastError.
+ *   - thread safety: no global mutable state; safe from any host thread.
+ */
+#ifndef SLDM_SAGE_H
+#define SLDM_SAGE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SLDM_ABI_VERSION 1
+
+enum sldm_dtype { SLDM_F32 = 0, SLDM_BF16 = 1 };
+enum sldm_status { SLDM_OK = 0, SLDM_ERR_ARG = 1, SLDM_ERR_HIP = 2 };
+
+/* ABI version compiled into the library (== SLDM_ABI_VERSION). */
+int sldm_abi_version(void);
+/* Message of the last failed call on this host thread ("" if none). */
+const char* sldm_last_error(void);
+
+/* ---------------------------------------------------------------- graph ---
+ * CSR build.  Replaces the per-call addressing of PyG
+ * 2.7.0 MessagePassing.propagate (x.index_select(0, edge_index[0]) and the
+ * scatter at edge_index[1]; called from sageblock.py:18) with, built once:
+ *   rowptr[N+1], col[E]      CSR by destination: sources of node i's in-edges
+ *   t_rowptr[N+1], t_col[E]  CSR by source (transpose): destinations
+ * Within a row the entries keep the original edge order (stable), i.e. the
+ * order in which PyG's CPU scatter_add_ accumulates.
+ * edge_index is [2,E] (row 0 = source, row 1 = target), int64 if
+ * index_is_int64 else int32.  Any id outside [0,N) sets *bad_index_flag
+ * (device int32, caller-zeroed) to 1; outputs are then unspecified.
+ * Requires N < 2^31 and E < 2^31.  t_rowptr/t_col may be NULL (forward only). */
+size_t sldm_csr_workspace_bytes(int64_t num_edges, int64_t num_nodes);
+int sldm_csr_build(const void* edge_index, int index_is_int64, int64_t num_edges,
+                   int64_t num_nodes, int32_t* rowptr, int32_t* col,
+                   int32_t* t_rowptr, int32_t* t_col, int32_t* bad_index_flag,
+                   void* workspace, size_t workspace_bytes, void* stream);
+
+/* ----------------------------------------------------------- aggregation ---
+ * out[i,:] = (addend[i,:] if addend) + S_i   with
+ *   S_i = sum_{k in [rowptr[i], rowptr[i+1])} x[col[k], :]       (mean == 0)
+ *   S_i = that sum / max(1, rowptr[i+1]-rowptr[i])               (mean == 1)
+ * Sums are fp32, accumulated in CSR order (bit-identical to PyG's CPU
+ * scatter_add_ for fp32 input).
+ * Forward (mean=1, CSR by dst) replaces PyG 2.7.0 x.index_select(0, src) +
+ * MeanAggregation / utils.scatter(reduce='mean').
+ * Backward (mean=0, transpose CSR, x = inv_deg-prescaled dAgg, addend = the
+ * lin_r input gradient) replaces autograd's gather + index_add_ (A8).
+ * addend may be NULL; it has out's dtype. */
+int sldm_gather_rows(int x_dtype, const void* x, int64_t ldx,
+                     const int32_t* rowptr, const int32_t* col,
+                     int64_t num_rows, int64_t feat, int mean,
+                     const void* addend, int64_t ld_add,
+                     int out_dtype, void* out, int64_t ldo, void* stream);
+
+/* g[i,:] = d[i,:] / max(1, rowptr[i+1]-rowptr[i]), in place, dtype of d.
+ * Backward of the mean's division (A8) folded before the transpose sum. */
+int sldm_scale_rows_by_inv_deg(int dtype, void* d, int64_t ld, const int32_t* rowptr,
+                               int64_t num_rows, int64_t feat, void* stream);
+
+/* ------------------------------------------------------------------ post ---
+ * Forward of sageblock.py:11-13 fused with lin_l's bias (A6 epilogue, A7):
+ *   hb   = h + bias                        (bias may be NULL)
+ *   xhat = (hb - mean) * rstd,  rstd = 1/sqrt(var_biased + eps)
+ *   y    = xhat * gamma + beta
+ *   z    = y > 0 ? y : y * negative_slope  (ReLU: negative_slope = 0)
+ *   out  = dropout(z)   keep iff u(seed, i*feat+j) >= drop_p, scale 1/(1-drop_p); drop_p in [0,1]
+ * drop_p = 0 means Identity / eval mode.  xhat (out's dtype) and rstd (fp32)
+ * are saved for the backward when non-NULL. */
+int sldm_post_fwd(int h_dtype, const void* h, int64_t ldh, int64_t num_rows, int64_t feat,
+                  const float* bias, const float* gamma, const float* beta, float eps,
+                  float negative_slope, float drop_p, uint64_t seed,
+                  int out_dtype, void* out, void* xhat, float* rstd, void* stream);
+
+/* Backward of sldm_post_fwd (autograd of Dropout, LeakyReLU/ReLU, LayerNorm):
+ *   dh = rstd * (g - mean_j(g) - xhat * mean_j(g*xhat)),  g = dy*gamma
+ * col_partials[p, 0:F] += dy*xhat (dgamma), [p, F:2F] dy (dbeta),
+ * [p, 2F:3F] dh (d bias of lin_l), over the rows handled by partial p
+ * (num_partials in [1, 4096]); reduce with sldm_colsum. */
+int sldm_post_bwd(int dtype, const void* dout, const void* xhat, const float* rstd,
+                  int64_t num_rows, int64_t feat, const float* gamma, const float* beta,
+                  float negative_slope, float drop_p, uint64_t seed,
+                  int dh_dtype, void* dh, float* col_partials, int num_partials,
+                  void* stream);
+int sldm_post_num_partials(int64_t num_rows, int64_t feat);
+
+/* out[j] = sum_p partials[p*width + j], fixed order (deterministic). */
+int sldm_colsum(const float* partials, int num_partials, int64_t width, float* out,
+                void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SLDM_SAGE_H */

@@ -1,0 +1,152 @@
+// Shared helpers for the gfx950 kernels of libsldm_sage.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sldm_sage.h"
+
+namespace sldm {
+
+// Thread-local last-error message (sldm_last_error()).
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+void clear_error();
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+constexpr int kWave = 64;  // CDNA wavefront
+
+// ------------------------------------------------------------------ bf16 --
+__device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
+// Round-to-nearest-even; a plain cast lowers to v_cvt_pk_bf16_f32 on gfx950
+// and keeps NaN a NaN.
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+}
+
+// ------------------------------------------- vector load/store of V elems --
+// Loads V consecutive elements of T (float or uint16 bf16) into fp32 regs.
+template <typename T, int V> struct Vec;
+
+template <> struct Vec<float, 4> {
+  __device__ static void load(const float* p, float* r) {
+    float4 v = *reinterpret_cast<const float4*>(p);
+    r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+  }
+  __device__ static void store(float* p, const float* r) {
+    *reinterpret_cast<float4*>(p) = make_float4(r[0], r[1], r[2], r[3]);
+  }
+};
+template <> struct Vec<float, 2> {
+  __device__ static void load(const float* p, float* r) {
+    float2 v = *reinterpret_cast<const float2*>(p);
+    r[0] = v.x; r[1] = v.y;
+  }
+  __device__ static void store(float* p, const float* r) {
+    *reinterpret_cast<float2*>(p) = make_float2(r[0], r[1]);
+  }
+};
+template <> struct Vec<float, 1> {
+  __device__ static void load(const float* p, float* r) { r[0] = *p; }
+  __device__ static void store(float* p, const float* r) { *p = r[0]; }
+};
+template <> struct Vec<uint16_t, 8> {
+  __device__ static void load(const uint16_t* p, float* r) {
+    uint4 v = *reinterpret_cast<const uint4*>(p);
+    r[0] = bf16_lo(v.x); r[1] = bf16_hi(v.x); r[2] = bf16_lo(v.y); r[3] = bf16_hi(v.y);
+    r[4] = bf16_lo(v.z); r[5] = bf16_hi(v.z); r[6] = bf16_lo(v.w); r[7] = bf16_hi(v.w);
+  }
+  __device__ static void store(uint16_t* p, const float* r) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(pack_bf16x2(r[0], r[1]), pack_bf16x2(r[2], r[3]),
+                                              pack_bf16x2(r[4], r[5]), pack_bf16x2(r[6], r[7]));
+  }
+};
+template <> struct Vec<uint16_t, 4> {
+  __device__ static void load(const uint16_t* p, float* r) {
+    uint2 v = *reinterpret_cast<const uint2*>(p);
+    r[0] = bf16_lo(v.x); r[1] = bf16_hi(v.x); r[2] = bf16_lo(v.y); r[3] = bf16_hi(v.y);
+  }
+  __device__ static void store(uint16_t* p, const float* r) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf16x2(r[0], r[1]), pack_bf16x2(r[2], r[3]));
+  }
+};
+template <> struct Vec<uint16_t, 2> {
+  __device__ static void load(const uint16_t* p, float* r) {
+    uint32_t v = *reinterpret_cast<const uint32_t*>(p);
+    r[0] = bf16_lo(v); r[1] = bf16_hi(v);
+  }
+  __device__ static void store(uint16_t* p, const float* r) {
+    *reinterpret_cast<uint32_t*>(p) = pack_bf16x2(r[0], r[1]);
+  }
+};
+template <> struct Vec<uint16_t, 1> {
+  __device__ static void load(const uint16_t* p, float* r) { r[0] = bf16_to_f32(*p); }
+  __device__ static void store(uint16_t* p, const float* r) { *p = f32_to_bf16(r[0]); }
+};
+
+// Widest element count V (16 B max per lane) such that feat, the leading
+// dimensions and the base pointers keep every V-vector naturally aligned.
+inline int pick_vec(int elem_bytes, int64_t feat, std::initializer_list<int64_t> lds,
+                    std::initializer_list<const void*> ptrs) {
+  int v = 16 / elem_bytes;
+  for (; v > 1; v >>= 1) {
+    bool ok = (feat % v) == 0;
+    for (int64_t ld : lds) ok = ok && (ld % v) == 0;
+    for (const void* p : ptrs)
+      ok = ok && (p == nullptr || (reinterpret_cast<uintptr_t>(p) % (size_t)(v * elem_bytes)) == 0);
+    if (ok) break;
+  }
+  return v;
+}
+
+// Lanes that share one row: next power of two >= feat/V, capped at one wave.
+inline int lanes_per_row(int64_t feat, int v) {
+  int64_t need = (feat + v - 1) / v;
+  int l = 1;
+  while (l < need && l < kWave) l <<= 1;
+  return l;
+}
+
+// Counter-based dropout uniform in [0,1): splitmix64 finaliser of (seed, idx).
+__device__ __forceinline__ float dropout_uniform(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+}  // namespace sldm
+
+#define SLDM_REQUIRE(cond, ...)          \
+  do {                                   \
+    if (!(cond)) {                       \
+      ::sldm::set_error(__VA_ARGS__);    \
+      return SLDM_ERR_ARG;               \
+    }                                    \
+  } while (0)
+
+#define SLDM_LAUNCH_CHECK(name)                                                   \
+  do {                                                                            \
+    hipError_t e_ = hipGetLastError();                                            \
+    if (e_ != hipSuccess) {                                                       \
+      ::sldm::set_error("%s: launch failed: %s", name, hipGetErrorString(e_));   \
+      return SLDM_ERR_HIP;                                                        \
+    }                                                                             \
+  } while (0)
+
+#define SLDM_HIP_CHECK(expr)                                                      \
+  do {                                                                            \
+    hipError_t e_ = (expr);                                                       \
+    if (e_ != hipSuccess) {                                                       \
+      ::sldm::set_error("%s: %s", #expr, hipGetErrorString(e_));                  \
+      return SLDM_ERR_HIP;                                                        \
+    }                                                                             \
+  } while (0)

@@ -1,0 +1,247 @@
+// CSR row gather: the SageBlock neighbour aggregation
+// and its transpose for the backward (A8).
+//
+// Replaces, per SAGEConv call (sageblock.py:18 -> PyG 2.7.0 propagate):
+//   x_j = x.index_select(0, edge_index[0])              [E,F] message tensor
+//   agg = scatter_add_(dst, x_j) / count.clamp(min=1)   MeanAggregation
+// without materialising the [E,F] messages: each destination row is summed
+// straight from the source rows it names.
+//
+// Layout / mapping (HBM-bound; algorithmic bytes per call
+//   B = E*(4 + F*s) + (N+1)*4 + N*F*s_out [+ N*F*s_add]):
+//   - a row is owned by LPR lanes (power of two, <= one wave64); each lane
+//     holds V consecutive features (16 B: 4 fp32 or 8 bf16) per chunk, NCH
+//     chunks per lane when a row is wider than a wave's 1 KiB;
+//   - every source row is read as whole 16-B-per-lane vectors: a bf16 F=256
+//     row is 512 B = one coalesced half-wave load; two rows share a wave;
+//   - up to 8 source rows per row-group are in flight before the first
+//     accumulate (batches of 8/4/2/1, no per-element predication, so the
+//     compiler keeps the loads un-waited);
+//   - fp32 accumulation in CSR order -> bit-identical to the reference's CPU
+//     scatter_add_ for fp32 input; the mean divides by the fp32 degree
+//     (PyG divides by the fp32 count).
+#include "common.hpp"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+template <typename TI, typename TO, int V, int NCH, bool MEAN, bool ADD>
+__global__ __launch_bounds__(kBlock) void gather_rows_kernel(
+    const TI* __restrict__ x, int64_t ldx, const int32_t* __restrict__ rowptr,
+    const int32_t* __restrict__ col, int64_t nrows, int feat, int lpr_log2,
+    const TO* __restrict__ addend, int64_t lda, TO* __restrict__ out, int64_t ldo) {
+  const int lpr = 1 << lpr_log2;
+  const int lane_in_row = threadIdx.x & (lpr - 1);
+  const int64_t row = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> lpr_log2;
+  if (row >= nrows) return;
+
+  int f0[NCH];
+  bool act[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    int f = (lane_in_row + c * lpr) * V;
+    act[c] = f < feat;
+    f0[c] = act[c] ? f : feat - V;  // clamp: inactive lanes re-read a valid vector
+  }
+
+  float acc[NCH][V];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[c][v] = 0.0f;
+
+  const int beg = rowptr[row];
+  const int end = rowptr[row + 1];
+
+  auto batch = [&](int k, auto u_const) {
+    constexpr int U = decltype(u_const)::value;
+    int idx[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) idx[u] = col[k + u];
+    float d[U][NCH][V];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+        sldm::Vec<TI, V>::load(x + (int64_t)idx[u] * ldx + f0[c], d[u][c]);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[c][v] += d[u][c][v];
+  };
+
+  int k = beg;
+  for (; k + 8 <= end; k += 8) batch(k, std::integral_constant<int, 8>{});
+  if (k + 4 <= end) { batch(k, std::integral_constant<int, 4>{}); k += 4; }
+  if (k + 2 <= end) { batch(k, std::integral_constant<int, 2>{}); k += 2; }
+  if (k < end) batch(k, std::integral_constant<int, 1>{});
+
+  if (MEAN) {
+    const float cnt = (float)(end - beg > 0 ? end - beg : 1);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[c][v] = acc[c][v] / cnt;
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    if (!act[c]) continue;
+    if (ADD) {
+      float a[V];
+      sldm::Vec<TO, V>::load(addend + row * lda + f0[c], a);
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[c][v] = a[v] + acc[c][v];
+    }
+    sldm::Vec<TO, V>::store(out + row * ldo + f0[c], acc[c]);
+  }
+}
+
+template <typename TI, typename TO, int V, bool MEAN, bool ADD>
+int launch_nch(const TI* x, int64_t ldx, const int32_t* rowptr, const int32_t* col,
+               int64_t nrows, int feat, const TO* addend, int64_t lda, TO* out, int64_t ldo,
+               hipStream_t stream) {
+  int lpr = sldm::lanes_per_row(feat, V);
+  int lpr_log2 = 0;
+  while ((1 << lpr_log2) < lpr) ++lpr_log2;
+  const int64_t nch = (feat + (int64_t)lpr * V - 1) / ((int64_t)lpr * V);
+  const int64_t threads = nrows << lpr_log2;
+  const int64_t grid = (threads + kBlock - 1) / kBlock;
+  SLDM_REQUIRE(grid < ((int64_t)1 << 31), "sldm_gather_rows: grid too large");
+#define SLDM_GATHER_CASE(NC)                                                            \
+  case NC:                                                                              \
+    gather_rows_kernel<TI, TO, V, NC, MEAN, ADD><<<(unsigned)grid, kBlock, 0, stream>>>( \
+        x, ldx, rowptr, col, nrows, feat, lpr_log2, addend, lda, out, ldo);             \
+    break;
+  switch (nch) {
+    SLDM_GATHER_CASE(1)
+    SLDM_GATHER_CASE(2)
+    SLDM_GATHER_CASE(3)
+    SLDM_GATHER_CASE(4)
+    default:
+      sldm::set_error("sldm_gather_rows: feat=%d too wide (max %d)", feat, 4 * 64 * V);
+      return SLDM_ERR_ARG;
+  }
+#undef SLDM_GATHER_CASE
+  SLDM_LAUNCH_CHECK("gather_rows_kernel");
+  return SLDM_OK;
+}
+
+template <typename TI, typename TO, bool MEAN, bool ADD>
+int launch_vec(int v, const void* x, int64_t ldx, const int32_t* rowptr, const int32_t* col,
+               int64_t nrows, int feat, const void* addend, int64_t lda, void* out, int64_t ldo,
+               hipStream_t stream) {
+  auto xi = reinterpret_cast<const TI*>(x);
+  auto ad = reinterpret_cast<const TO*>(addend);
+  auto o = reinterpret_cast<TO*>(out);
+  switch (v) {
+    case 8:
+      if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2)
+        return launch_nch<TI, TO, 8, MEAN, ADD>(xi, ldx, rowptr, col, nrows, feat, ad, lda, o, ldo, stream);
+      break;
+    case 4:
+      return launch_nch<TI, TO, 4, MEAN, ADD>(xi, ldx, rowptr, col, nrows, feat, ad, lda, o, ldo, stream);
+    case 2:
+      return launch_nch<TI, TO, 2, MEAN, ADD>(xi, ldx, rowptr, col, nrows, feat, ad, lda, o, ldo, stream);
+    case 1:
+      return launch_nch<TI, TO, 1, MEAN, ADD>(xi, ldx, rowptr, col, nrows, feat, ad, lda, o, ldo, stream);
+  }
+  sldm::set_error("sldm_gather_rows: unsupported vector width %d", v);
+  return SLDM_ERR_ARG;
+}
+
+template <typename T, bool MEAN, bool ADD>
+int dispatch_same(const void* x, int64_t ldx, const int32_t* rowptr, const int32_t* col,
+                  int64_t nrows, int feat, const void* addend, int64_t lda, void* out,
+                  int64_t ldo, hipStream_t stream) {
+  int v = sldm::pick_vec((int)sizeof(T), feat, {ldx, ldo, ADD ? lda : (int64_t)0},
+                         {x, out, addend});
+  return launch_vec<T, T, MEAN, ADD>(v, x, ldx, rowptr, col, nrows, feat, addend, lda, out, ldo,
+                                     stream);
+}
+
+}  // namespace
+
+extern "C" int sldm_gather_rows(int x_dtype, const void* x, int64_t ldx, const int32_t* rowptr,
+                                const int32_t* col, int64_t num_rows, int64_t feat, int mean,
+                                const void* addend, int64_t ld_add, int out_dtype, void* out,
+                                int64_t ldo, void* stream_) {
+  SLDM_REQUIRE(x_dtype == out_dtype && (x_dtype == SLDM_F32 || x_dtype == SLDM_BF16),
+               "sldm_gather_rows: dtypes (%d -> %d) unsupported: both F32 or both BF16",
+               x_dtype, out_dtype);
+  SLDM_REQUIRE(num_rows >= 0 && feat >= 0 && feat < (1 << 20),
+               "sldm_gather_rows: bad sizes rows=%lld feat=%lld", (long long)num_rows,
+               (long long)feat);
+  if (num_rows == 0 || feat == 0) return SLDM_OK;
+  SLDM_REQUIRE(x && rowptr && col && out, "sldm_gather_rows: NULL pointer argument");
+  SLDM_REQUIRE(ldx >= feat && ldo >= feat && (!addend || ld_add >= feat),
+               "sldm_gather_rows: leading dimension smaller than feat");
+  hipStream_t stream = sldm::as_stream(stream_);
+  const int f = (int)feat;
+  const bool add = addend != nullptr;
+  if (x_dtype == SLDM_F32) {
+    if (mean)
+      return add ? dispatch_same<float, true, true>(x, ldx, rowptr, col, num_rows, f, addend, ld_add, out, ldo, stream)
+                 : dispatch_same<float, true, false>(x, ldx, rowptr, col, num_rows, f, addend, ld_add, out, ldo, stream);
+    return add ? dispatch_same<float, false, true>(x, ldx, rowptr, col, num_rows, f, addend, ld_add, out, ldo, stream)
+               : dispatch_same<float, false, false>(x, ldx, rowptr, col, num_rows, f, addend, ld_add, out, ldo, stream);
+  }
+  if (mean)
+    return add ? dispatch_same<uint16_t, true, true>(x, ldx, rowptr, col, num_rows, f, addend, ld_add, out, ldo, stream)
+               : dispatch_same<uint16_t, true, false>(x, ldx, rowptr, col, num_rows, f, addend, ld_add, out, ldo, stream);
+  return add ? dispatch_same<uint16_t, false, true>(x, ldx, rowptr, col, num_rows, f, addend, ld_add, out, ldo, stream)
+             : dispatch_same<uint16_t, false, false>(x, ldx, rowptr, col, num_rows, f, addend, ld_add, out, ldo, stream);
+}
+
+// ------------------------------------------------------------------------
+namespace {
+template <typename T, int V>
+__global__ __launch_bounds__(kBlock) void scale_inv_deg_kernel(T* __restrict__ d, int64_t ld,
+                                                               const int32_t* __restrict__ rowptr,
+                                                               int64_t nrows, int feat) {
+  const int64_t vecs_per_row = feat / V;
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= nrows * vecs_per_row) return;
+  const int64_t row = i / vecs_per_row;
+  const int64_t f = (i - row * vecs_per_row) * V;
+  const int deg = rowptr[row + 1] - rowptr[row];
+  const float cnt = (float)(deg > 0 ? deg : 1);
+  float r[V];
+  sldm::Vec<T, V>::load(d + row * ld + f, r);
+#pragma unroll
+  for (int v = 0; v < V; ++v) r[v] = r[v] / cnt;
+  sldm::Vec<T, V>::store(d + row * ld + f, r);
+}
+
+template <typename T>
+int launch_scale(void* d, int64_t ld, const int32_t* rowptr, int64_t nrows, int feat,
+                 hipStream_t stream) {
+  int v = sldm::pick_vec((int)sizeof(T), feat, {ld}, {d});
+  auto p = reinterpret_cast<T*>(d);
+  const int64_t n = nrows * (feat / v);
+  const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
+  switch (v) {
+    case 8:
+      if constexpr (sizeof(T) == 2) scale_inv_deg_kernel<T, 8><<<grid, kBlock, 0, stream>>>(p, ld, rowptr, nrows, feat);
+      break;
+    case 4: scale_inv_deg_kernel<T, 4><<<grid, kBlock, 0, stream>>>(p, ld, rowptr, nrows, feat); break;
+    case 2: scale_inv_deg_kernel<T, 2><<<grid, kBlock, 0, stream>>>(p, ld, rowptr, nrows, feat); break;
+    default: scale_inv_deg_kernel<T, 1><<<grid, kBlock, 0, stream>>>(p, ld, rowptr, nrows, feat); break;
+  }
+  SLDM_LAUNCH_CHECK("scale_inv_deg_kernel");
+  return SLDM_OK;
+}
+}  // namespace
+
+extern "C" int sldm_scale_rows_by_inv_deg(int dtype, void* d, int64_t ld, const int32_t* rowptr,
+                                          int64_t num_rows, int64_t feat, void* stream_) {
+  SLDM_REQUIRE(dtype == SLDM_F32 || dtype == SLDM_BF16, "sldm_scale_rows_by_inv_deg: dtype %d",
+               dtype);
+  if (num_rows <= 0 || feat <= 0) return SLDM_OK;
+  SLDM_REQUIRE(d && rowptr && ld >= feat, "sldm_scale_rows_by_inv_deg: bad arguments");
+  hipStream_t stream = sldm::as_stream(stream_);
+  return dtype == SLDM_F32 ? launch_scale<float>(d, ld, rowptr, num_rows, (int)feat, stream)
+                           : launch_scale<uint16_t>(d, ld, rowptr, num_rows, (int)feat, stream);
+}

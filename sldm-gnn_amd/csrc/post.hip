@@ -1,0 +1,384 @@
+// Post-conv elementwise stage of a SageBlock layer (SURVEY.md §8a A6 epilogue +
+// A7): lin_l bias -> LayerNorm(F_out, eps) -> LeakyReLU(ns)/ReLU -> Dropout(p),
+// /root/reference/src/models/blocks/sageblock.py:9-15, and its backward (A8).
+//
+// Row-wise and HBM-bound: a row is owned by LPR lanes (power of two <= 64),
+// each holding NCH x V consecutive features in registers, so the LayerNorm
+// statistics need only lane shuffles (two-pass mean / variance in fp32).
+// Dropout uses a counter-based hash of (seed, row*F + col) so the backward
+// regenerates the mask instead of storing it.
+#include "common.hpp"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ float group_sum(float v, int lpr) {
+  for (int off = lpr >> 1; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <typename TH, typename TO, int V, int NCH>
+__global__ __launch_bounds__(kBlock) void post_fwd_kernel(
+    const TH* __restrict__ h, int64_t ldh, int64_t nrows, int feat, int lpr_log2,
+    const float* __restrict__ bias, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float slope, float drop_p, float drop_scale,
+    uint64_t seed, TO* __restrict__ out, TO* __restrict__ xhat_out, float* __restrict__ rstd_out) {
+  const int lpr = 1 << lpr_log2;
+  const int lane_in_row = threadIdx.x & (lpr - 1);
+  const int64_t row = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> lpr_log2;
+  const bool live = row < nrows;  // dead lanes still take part in the shuffles
+  const int64_t r = live ? row : 0;
+
+  int f0[NCH];
+  bool act[NCH];
+  float v[NCH][V];
+  float sum = 0.0f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    int f = (lane_in_row + c * lpr) * V;
+    act[c] = f < feat;
+    f0[c] = act[c] ? f : feat - V;
+    sldm::Vec<TH, V>::load(h + r * ldh + f0[c], v[c]);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      if (bias) v[c][k] += bias[f0[c] + k];
+      if (!act[c]) v[c][k] = 0.0f;
+      sum += v[c][k];
+    }
+  }
+  const float inv_f = 1.0f / (float)feat;
+  const float mean = group_sum(sum, lpr) * inv_f;
+  float sq = 0.0f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      float dlt = act[c] ? v[c][k] - mean : 0.0f;
+      sq += dlt * dlt;
+    }
+  const float var = group_sum(sq, lpr) * inv_f;
+  const float rstd = 1.0f / sqrtf(var + eps);
+  if (!live) return;
+  if (rstd_out && lane_in_row == 0) rstd_out[row] = rstd;
+
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    if (!act[c]) continue;
+    float xh[V], z[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const int f = f0[c] + k;
+      xh[k] = (v[c][k] - mean) * rstd;
+      float y = xh[k] * gamma[f] + beta[f];
+      float a = y > 0.0f ? y : y * slope;
+      if (drop_p > 0.0f) {
+        float u = sldm::dropout_uniform(seed, (uint64_t)row * (uint64_t)feat + (uint64_t)f);
+        a = (u >= drop_p) ? a * drop_scale : 0.0f;
+      }
+      z[k] = a;
+    }
+    sldm::Vec<TO, V>::store(out + row * (int64_t)feat + f0[c], z);
+    if (xhat_out) sldm::Vec<TO, V>::store(xhat_out + row * (int64_t)feat + f0[c], xh);
+  }
+}
+
+// One block per partial; grid-stride over row groups.  Column partials are
+// kept per thread (fixed columns), then combined across the block's row
+// groups in LDS and written as partials[blockIdx.x][3][feat].
+template <typename T, typename TD, int V, int NCH>
+__global__ __launch_bounds__(kBlock) void post_bwd_kernel(
+    const T* __restrict__ dout, const T* __restrict__ xhat, const float* __restrict__ rstd,
+    int64_t nrows, int feat, int lpr_log2, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float slope, float drop_p, float drop_scale, uint64_t seed,
+    TD* __restrict__ dh, float* __restrict__ partials) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [kBlock/lpr][3][feat] reused
+  const int lpr = 1 << lpr_log2;
+  const int lane_in_row = threadIdx.x & (lpr - 1);
+  const int group = threadIdx.x >> lpr_log2;
+  const int groups_per_block = kBlock >> lpr_log2;
+
+  int f0[NCH];
+  bool act[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    int f = (lane_in_row + c * lpr) * V;
+    act[c] = f < feat;
+    f0[c] = act[c] ? f : feat - V;
+  }
+  float pg[NCH][V], pb[NCH][V], pd[NCH][V];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int k = 0; k < V; ++k) pg[c][k] = pb[c][k] = pd[c][k] = 0.0f;
+
+  const float inv_f = 1.0f / (float)feat;
+  const int64_t stride = (int64_t)gridDim.x * groups_per_block;
+  const int64_t nrounds = (nrows + stride - 1) / stride;
+  for (int64_t it = 0; it < nrounds; ++it) {
+    const int64_t row = it * stride + (int64_t)blockIdx.x * groups_per_block + group;
+    const bool live = row < nrows;
+    const int64_t r = live ? row : 0;
+    const float rs = rstd[r];
+    float xh[NCH][V], gx[NCH][V], dy[NCH][V];
+    float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      float go[V];
+      sldm::Vec<T, V>::load(dout + r * (int64_t)feat + f0[c], go);
+      sldm::Vec<T, V>::load(xhat + r * (int64_t)feat + f0[c], xh[c]);
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const int f = f0[c] + k;
+        const float g = gamma[f];
+        const float y = xh[c][k] * g + beta[f];
+        float d = go[k];
+        if (drop_p > 0.0f) {
+          float u = sldm::dropout_uniform(seed, (uint64_t)r * (uint64_t)feat + (uint64_t)f);
+          d = (u >= drop_p) ? d * drop_scale : 0.0f;
+        }
+        d = y > 0.0f ? d : d * slope;
+        if (!act[c] || !live) { d = 0.0f; xh[c][k] = 0.0f; }
+        dy[c][k] = d;
+        gx[c][k] = d * g;
+        s1 += gx[c][k];
+        s2 += gx[c][k] * xh[c][k];
+      }
+    }
+    const float m1 = group_sum(s1, lpr) * inv_f;
+    const float m2 = group_sum(s2, lpr) * inv_f;
+    if (!live) continue;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if (!act[c]) continue;
+      float o[V];
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        o[k] = rs * (gx[c][k] - m1 - xh[c][k] * m2);
+        pg[c][k] += dy[c][k] * xh[c][k];
+        pb[c][k] += dy[c][k];
+        pd[c][k] += o[k];
+      }
+      sldm::Vec<TD, V>::store(dh + r * (int64_t)feat + f0[c], o);
+    }
+  }
+
+  // Block reduction of the column partials: groups_per_block rows of [3][feat].
+  float* mine = red + (size_t)group * 3 * feat;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    if (!act[c]) continue;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      mine[f0[c] + k] = pg[c][k];
+      mine[feat + f0[c] + k] = pb[c][k];
+      mine[2 * feat + f0[c] + k] = pd[c][k];
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < 3 * feat; j += kBlock) {
+    float s = 0.0f;
+    for (int g = 0; g < groups_per_block; ++g) s += red[(size_t)g * 3 * feat + j];
+    partials[(size_t)blockIdx.x * 3 * feat + j] = s;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void colsum_kernel(const float* __restrict__ partials,
+                                                        int np, int64_t width,
+                                                        float* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= width) return;
+  float s = 0.0f;
+  for (int p = 0; p < np; ++p) s += partials[(int64_t)p * width + j];
+  out[j] = s;
+}
+
+struct RowGeom {
+  int v, lpr, lpr_log2, nch;
+};
+
+RowGeom row_geom(int elem_bytes, int64_t feat, std::initializer_list<const void*> ptrs) {
+  RowGeom g;
+  g.v = sldm::pick_vec(elem_bytes, feat, {feat}, ptrs);
+  g.lpr = sldm::lanes_per_row(feat, g.v);
+  g.lpr_log2 = 0;
+  while ((1 << g.lpr_log2) < g.lpr) ++g.lpr_log2;
+  g.nch = (int)((feat + (int64_t)g.lpr * g.v - 1) / ((int64_t)g.lpr * g.v));
+  return g;
+}
+
+template <typename TH, typename TO, int V>
+int post_fwd_nch(const RowGeom& g, const void* h, int64_t ldh, int64_t nrows, int feat,
+                 const float* bias, const float* gamma, const float* beta, float eps,
+                 float slope, float p, float scale, uint64_t seed, void* out, void* xhat,
+                 float* rstd, hipStream_t stream) {
+  const int64_t grid = ((nrows << g.lpr_log2) + kBlock - 1) / kBlock;
+#define SLDM_PF_CASE(NC)                                                                     \
+  case NC:                                                                                   \
+    post_fwd_kernel<TH, TO, V, NC><<<(unsigned)grid, kBlock, 0, stream>>>(                   \
+        reinterpret_cast<const TH*>(h), ldh, nrows, feat, g.lpr_log2, bias, gamma, beta,     \
+        eps, slope, p, scale, seed, reinterpret_cast<TO*>(out), reinterpret_cast<TO*>(xhat), \
+        rstd);                                                                               \
+    break;
+  switch (g.nch) {
+    SLDM_PF_CASE(1)
+    SLDM_PF_CASE(2)
+    SLDM_PF_CASE(4)
+    default:
+      sldm::set_error("sldm_post_fwd: feat=%d unsupported (chunks %d)", feat, g.nch);
+      return SLDM_ERR_ARG;
+  }
+#undef SLDM_PF_CASE
+  SLDM_LAUNCH_CHECK("post_fwd_kernel");
+  return SLDM_OK;
+}
+
+template <typename T, typename TD, int V>
+int post_bwd_nch(const RowGeom& g, const void* dout, const void* xhat, const float* rstd,
+                 int64_t nrows, int feat, const float* gamma, const float* beta, float slope,
+                 float p, float scale, uint64_t seed, void* dh, float* partials, int np,
+                 hipStream_t stream) {
+  const size_t lds = sizeof(float) * 3 * (size_t)feat * (kBlock >> g.lpr_log2);
+  if (lds > 160 * 1024) {
+    sldm::set_error("sldm_post_bwd: feat=%d needs %zu B of LDS", feat, lds);
+    return SLDM_ERR_ARG;
+  }
+#define SLDM_PB_CASE(NC)                                                                       \
+  case NC:                                                                                     \
+    post_bwd_kernel<T, TD, V, NC><<<np, kBlock, lds, stream>>>(                                \
+        reinterpret_cast<const T*>(dout), reinterpret_cast<const T*>(xhat), rstd, nrows, feat, \
+        g.lpr_log2, gamma, beta, slope, p, scale, seed, reinterpret_cast<TD*>(dh), partials);  \
+    break;
+  switch (g.nch) {
+    SLDM_PB_CASE(1)
+    SLDM_PB_CASE(2)
+    SLDM_PB_CASE(4)
+    default:
+      sldm::set_error("sldm_post_bwd: feat=%d unsupported (chunks %d)", feat, g.nch);
+      return SLDM_ERR_ARG;
+  }
+#undef SLDM_PB_CASE
+  SLDM_LAUNCH_CHECK("post_bwd_kernel");
+  return SLDM_OK;
+}
+
+template <typename TH, typename TO>
+int post_fwd_t(const RowGeom& g, const void* h, int64_t ldh, int64_t nrows, int feat,
+               const float* bias, const float* gamma, const float* beta, float eps, float slope,
+               float p, float scale, uint64_t seed, void* out, void* xhat, float* rstd,
+               hipStream_t stream) {
+  switch (g.v) {
+    case 8:
+      if constexpr (sizeof(TH) == 2 && sizeof(TO) == 2)
+        return post_fwd_nch<TH, TO, 8>(g, h, ldh, nrows, feat, bias, gamma, beta, eps, slope, p, scale, seed, out, xhat, rstd, stream);
+      break;
+    case 4:
+      return post_fwd_nch<TH, TO, 4>(g, h, ldh, nrows, feat, bias, gamma, beta, eps, slope, p, scale, seed, out, xhat, rstd, stream);
+    case 2:
+      return post_fwd_nch<TH, TO, 2>(g, h, ldh, nrows, feat, bias, gamma, beta, eps, slope, p, scale, seed, out, xhat, rstd, stream);
+    case 1:
+      return post_fwd_nch<TH, TO, 1>(g, h, ldh, nrows, feat, bias, gamma, beta, eps, slope, p, scale, seed, out, xhat, rstd, stream);
+  }
+  sldm::set_error("sldm_post_fwd: vector width %d", g.v);
+  return SLDM_ERR_ARG;
+}
+
+template <typename T, typename TD>
+int post_bwd_t(const RowGeom& g, const void* dout, const void* xhat, const float* rstd,
+               int64_t nrows, int feat, const float* gamma, const float* beta, float slope,
+               float p, float scale, uint64_t seed, void* dh, float* partials, int np,
+               hipStream_t stream) {
+  switch (g.v) {
+    case 8:
+      if constexpr (sizeof(T) == 2 && sizeof(TD) == 2)
+        return post_bwd_nch<T, TD, 8>(g, dout, xhat, rstd, nrows, feat, gamma, beta, slope, p, scale, seed, dh, partials, np, stream);
+      break;
+    case 4:
+      return post_bwd_nch<T, TD, 4>(g, dout, xhat, rstd, nrows, feat, gamma, beta, slope, p, scale, seed, dh, partials, np, stream);
+    case 2:
+      return post_bwd_nch<T, TD, 2>(g, dout, xhat, rstd, nrows, feat, gamma, beta, slope, p, scale, seed, dh, partials, np, stream);
+    case 1:
+      return post_bwd_nch<T, TD, 1>(g, dout, xhat, rstd, nrows, feat, gamma, beta, slope, p, scale, seed, dh, partials, np, stream);
+  }
+  sldm::set_error("sldm_post_bwd: vector width %d", g.v);
+  return SLDM_ERR_ARG;
+}
+
+}  // namespace
+
+extern "C" int sldm_post_fwd(int h_dtype, const void* h, int64_t ldh, int64_t num_rows,
+                             int64_t feat, const float* bias, const float* gamma,
+                             const float* beta, float eps, float negative_slope, float drop_p,
+                             uint64_t seed, int out_dtype, void* out, void* xhat, float* rstd,
+                             void* stream_) {
+  SLDM_REQUIRE(num_rows >= 0 && feat > 0 && feat <= 4096, "sldm_post_fwd: bad sizes");
+  if (num_rows == 0) return SLDM_OK;
+  SLDM_REQUIRE(h && gamma && beta && out && ldh >= feat, "sldm_post_fwd: bad arguments");
+  SLDM_REQUIRE(drop_p >= 0.0f && drop_p <= 1.0f, "sldm_post_fwd: drop_p=%g outside [0,1]",
+               (double)drop_p);
+  const float scale = drop_p >= 1.0f ? 0.0f : (drop_p > 0.0f ? 1.0f / (1.0f - drop_p) : 1.0f);
+  hipStream_t stream = sldm::as_stream(stream_);
+  const int f = (int)feat;
+  int hb = h_dtype == SLDM_F32 ? 4 : 2, ob = out_dtype == SLDM_F32 ? 4 : 2;
+  RowGeom g = row_geom(hb > ob ? ob : hb, feat, {h, out, xhat});
+  if (h_dtype == SLDM_F32 || out_dtype == SLDM_F32) {
+    // Vector width is shared between input and output: cap it at 4.
+    if (g.v > 4) { g = row_geom(4, feat, {h, out, xhat}); }
+  }
+  SLDM_REQUIRE(ldh % g.v == 0, "sldm_post_fwd: ldh not aligned");
+  if (h_dtype == SLDM_F32 && out_dtype == SLDM_F32)
+    return post_fwd_t<float, float>(g, h, ldh, num_rows, f, bias, gamma, beta, eps, negative_slope, drop_p, scale, seed, out, xhat, rstd, stream);
+  if (h_dtype == SLDM_BF16 && out_dtype == SLDM_BF16)
+    return post_fwd_t<uint16_t, uint16_t>(g, h, ldh, num_rows, f, bias, gamma, beta, eps, negative_slope, drop_p, scale, seed, out, xhat, rstd, stream);
+  if (h_dtype == SLDM_F32 && out_dtype == SLDM_BF16)
+    return post_fwd_t<float, uint16_t>(g, h, ldh, num_rows, f, bias, gamma, beta, eps, negative_slope, drop_p, scale, seed, out, xhat, rstd, stream);
+  sldm::set_error("sldm_post_fwd: dtype pair (%d -> %d) unsupported", h_dtype, out_dtype);
+  return SLDM_ERR_ARG;
+}
+
+extern "C" int sldm_post_num_partials(int64_t num_rows, int64_t feat) {
+  if (num_rows <= 0 || feat <= 0) return 1;
+  RowGeom g = row_geom(4, feat, {});
+  const int64_t groups = kBlock >> g.lpr_log2;
+  int64_t np = (num_rows + groups * 4 - 1) / (groups * 4);  // >= 4 rows per group
+  if (np > 2048) np = 2048;
+  return (int)(np < 1 ? 1 : np);
+}
+
+extern "C" int sldm_post_bwd(int dtype, const void* dout, const void* xhat, const float* rstd,
+                             int64_t num_rows, int64_t feat, const float* gamma,
+                             const float* beta, float negative_slope, float drop_p,
+                             uint64_t seed, int dh_dtype, void* dh, float* col_partials,
+                             int num_partials, void* stream_) {
+  SLDM_REQUIRE(feat > 0 && feat <= 4096 && num_rows >= 0, "sldm_post_bwd: bad sizes");
+  SLDM_REQUIRE(num_partials >= 1 && num_partials <= 4096, "sldm_post_bwd: num_partials=%d",
+               num_partials);
+  SLDM_REQUIRE(dout && xhat && rstd && gamma && beta && dh && col_partials,
+               "sldm_post_bwd: NULL argument");
+  SLDM_REQUIRE(drop_p >= 0.0f && drop_p <= 1.0f, "sldm_post_bwd: drop_p=%g outside [0,1]",
+               (double)drop_p);
+  const float scale = drop_p >= 1.0f ? 0.0f : (drop_p > 0.0f ? 1.0f / (1.0f - drop_p) : 1.0f);
+  hipStream_t stream = sldm::as_stream(stream_);
+  const int f = (int)feat;
+  int eb = (dtype == SLDM_F32 || dh_dtype == SLDM_F32) ? 4 : 2;
+  RowGeom g = row_geom(eb, feat, {dout, xhat, dh});
+  if (dtype == SLDM_F32 && dh_dtype == SLDM_F32)
+    return post_bwd_t<float, float>(g, dout, xhat, rstd, num_rows, f, gamma, beta, negative_slope, drop_p, scale, seed, dh, col_partials, num_partials, stream);
+  if (dtype == SLDM_BF16 && dh_dtype == SLDM_BF16)
+    return post_bwd_t<uint16_t, uint16_t>(g, dout, xhat, rstd, num_rows, f, gamma, beta, negative_slope, drop_p, scale, seed, dh, col_partials, num_partials, stream);
+  if (dtype == SLDM_BF16 && dh_dtype == SLDM_F32)
+    return post_bwd_t<uint16_t, float>(g, dout, xhat, rstd, num_rows, f, gamma, beta, negative_slope, drop_p, scale, seed, dh, col_partials, num_partials, stream);
+  sldm::set_error("sldm_post_bwd: dtype pair (%d, dh %d) unsupported", dtype, dh_dtype);
+  return SLDM_ERR_ARG;
+}
+
+extern "C" int sldm_colsum(const float* partials, int num_partials, int64_t width, float* out,
+                           void* stream_) {
+  SLDM_REQUIRE(num_partials >= 1 && width >= 0 && partials && out, "sldm_colsum: bad arguments");
+  if (width == 0) return SLDM_OK;
+  hipStream_t stream = sldm::as_stream(stream_);
+  colsum_kernel<<<(unsigned)((width + kBlock - 1) / kBlock), kBlock, 0, stream>>>(
+      partials, num_partials, width, out);
+  SLDM_LAUNCH_CHECK("colsum_kernel");
+  return SLDM_OK;
+}

@@ -1,0 +1,193 @@
+"""Tensor-level wrappers over the C ABI (device pointers + the current HIP stream).
+
+Every op here launches a hand-written gfx950 kernel of libsldm_sage.so on
+``torch.cuda.current_stream()``; outputs are allocated through the PyTorch
+caching allocator.  CPU tensors are rejected: there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+_DTYPE_CODE = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16}
+
+# Optional per-kernel timing hook used by bench.py: a callable
+# ``(name, start_event, end_event, units)`` or None.
+_timing_hook = None
+
+
+def set_timing_hook(hook) -> None:
+    global _timing_hook
+    _timing_hook = hook
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    try:
+        return _DTYPE_CODE[t.dtype]
+    except KeyError:
+        raise TypeError(f"sldm_sage: unsupported dtype {t.dtype} (float32 or bfloat16)") from None
+
+
+def _require_gpu(*ts: torch.Tensor) -> torch.device:
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise RuntimeError(
+                "sldm_sage runs only on the GPU (HIP/gfx950); got a tensor on "
+                f"'{t.device}'. There is no CPU fallback: move the inputs and the module "
+                "to a ROCm device.")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"sldm_sage: tensors on different devices ({dev}, {t.device})")
+    return dev
+
+
+def _stream(dev: torch.device) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+class _Timed:
+    """Brackets one launch with HIP events when the timing hook is set."""
+
+    __slots__ = ("name", "units", "start")
+
+    def __init__(self, name: str, units: float):
+        self.name, self.units, self.start = name, units, None
+
+    def __enter__(self):
+        if _timing_hook is not None:
+            self.start = torch.cuda.Event(enable_timing=True)
+            self.start.record()
+        return self
+
+    def __exit__(self, *exc):
+        if self.start is not None and exc[0] is None:
+            end = torch.cuda.Event(enable_timing=True)
+            end.record()
+            _timing_hook(self.name, self.start, end, self.units)
+        return False
+
+
+# ------------------------------------------------------------------ graph --
+def csr_build(edge_index: torch.Tensor, num_nodes: int, transpose: bool = True):
+    """edge_index [2,E] (int64/int32, on the GPU) -> (rowptr, col, t_rowptr, t_col, bad).
+
+    ``bad`` is a 1-element int32 device tensor, nonzero if an id was outside
+    [0, num_nodes).  t_rowptr / t_col are None when ``transpose`` is False.
+    """
+    dev = _require_gpu(edge_index)
+    if edge_index.dim() != 2 or edge_index.size(0) != 2:
+        raise ValueError(f"edge_index must be [2, E], got {tuple(edge_index.shape)}")
+    if edge_index.dtype not in (torch.int64, torch.int32):
+        raise TypeError(f"edge_index must be int64 or int32, got {edge_index.dtype}")
+    ei = edge_index.contiguous()
+    E = ei.size(1)
+    N = int(num_nodes)
+    lib = _lib.load()
+    i32 = dict(dtype=torch.int32, device=dev)
+    rowptr = torch.empty(N + 1, **i32)
+    col = torch.empty(max(E, 1), **i32)[:E]
+    t_rowptr = torch.empty(N + 1, **i32) if transpose else None
+    t_col = torch.empty(max(E, 1), **i32)[:E] if transpose else None
+    bad = torch.zeros(1, **i32)
+    ws_bytes = lib.sldm_csr_workspace_bytes(E, N)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    with _Timed("csr_build", E):
+        _lib.check(lib.sldm_csr_build(ei.data_ptr(), int(ei.dtype == torch.int64), E, N,
+                                      rowptr.data_ptr(), col.data_ptr(), _ptr(t_rowptr),
+                                      _ptr(t_col), bad.data_ptr(), ws.data_ptr(), ws_bytes,
+                                      _stream(dev)),
+                   "sldm_csr_build")
+    return rowptr, col, t_rowptr, t_col, bad
+
+
+# ------------------------------------------------------------ aggregation --
+def gather_rows(x: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor, num_rows: int,
+                mean: bool, addend: torch.Tensor | None = None,
+                out: torch.Tensor | None = None, name: str = "gather") -> torch.Tensor:
+    """out[i] = (addend[i] +) sum_{k in row i} x[col[k]]  (/ max(1, deg_i) if mean)."""
+    dev = _require_gpu(x, rowptr, col, addend, out)
+    if x.dim() != 2 or x.stride(1) != 1:
+        x = x.contiguous()
+    F = x.size(1)
+    if out is None:
+        out = torch.empty(num_rows, F, dtype=x.dtype, device=dev)
+    if addend is not None:
+        if addend.dtype != out.dtype or addend.stride(-1) != 1:
+            addend = addend.to(out.dtype).contiguous()
+    if num_rows == 0 or F == 0:
+        return out
+    E = col.numel()
+    s = x.element_size()
+    bytes_alg = E * (4 + F * s) + (num_rows + 1) * 4 + num_rows * F * s * (2 if addend is not None else 1)
+    with _Timed(name, bytes_alg):
+        _lib.check(_lib.load().sldm_gather_rows(
+            dtype_code(x), x.data_ptr(), x.stride(0), rowptr.data_ptr(),
+            col.data_ptr() if E else rowptr.data_ptr(), num_rows, F, int(bool(mean)),
+            _ptr(addend), addend.stride(0) if addend is not None else 0,
+            dtype_code(out), out.data_ptr(), out.stride(0), _stream(dev)), "sldm_gather_rows")
+    return out
+
+
+def scale_rows_by_inv_deg_(d: torch.Tensor, rowptr: torch.Tensor) -> torch.Tensor:
+    dev = _require_gpu(d, rowptr)
+    assert d.stride(1) == 1
+    _lib.check(_lib.load().sldm_scale_rows_by_inv_deg(
+        dtype_code(d), d.data_ptr(), d.stride(0), rowptr.data_ptr(), d.size(0), d.size(1),
+        _stream(dev)), "sldm_scale_rows_by_inv_deg")
+    return d
+
+
+# ------------------------------------------------------------------- post --
+def post_fwd(h: torch.Tensor, bias, gamma, beta, eps: float, slope: float, drop_p: float,
+             seed: int, out_dtype: torch.dtype, save: bool):
+    """bias + LayerNorm + (Leaky)ReLU + dropout; returns (out, xhat|None, rstd|None)."""
+    dev = _require_gpu(h, gamma, beta, bias)
+    N, F = h.shape
+    if h.stride(1) != 1:
+        h = h.contiguous()
+    out = torch.empty(N, F, dtype=out_dtype, device=dev)
+    xhat = torch.empty(N, F, dtype=out_dtype, device=dev) if save else None
+    rstd = torch.empty(N, dtype=torch.float32, device=dev) if save else None
+    f32 = lambda t: None if t is None else t.detach().float().contiguous()  # noqa: E731
+    bias_, gamma_, beta_ = f32(bias), f32(gamma), f32(beta)
+    with _Timed("post_fwd", N * F * (h.element_size() + out.element_size() * (2 if save else 1))):
+        _lib.check(_lib.load().sldm_post_fwd(
+            dtype_code(h), h.data_ptr(), h.stride(0), N, F, _ptr(bias_), gamma_.data_ptr(),
+            beta_.data_ptr(), float(eps), float(slope), float(drop_p), seed & (2**64 - 1),
+            _DTYPE_CODE[out_dtype], out.data_ptr(), _ptr(xhat), _ptr(rstd), _stream(dev)),
+            "sldm_post_fwd")
+    return out, xhat, rstd
+
+
+def post_bwd(dout: torch.Tensor, xhat: torch.Tensor, rstd: torch.Tensor, gamma, beta,
+             slope: float, drop_p: float, seed: int, dh_dtype: torch.dtype):
+    """Returns (dh [N,F], dgamma [F], dbeta [F], dbias [F]) (the last three fp32)."""
+    dev = _require_gpu(dout, xhat, rstd)
+    N, F = xhat.shape
+    if dout.dtype != xhat.dtype or dout.stride(1) != 1 or dout.stride(0) != F:
+        dout = dout.to(xhat.dtype).contiguous()
+    lib = _lib.load()
+    np_ = lib.sldm_post_num_partials(N, F)
+    dh = torch.empty(N, F, dtype=dh_dtype, device=dev)
+    partials = torch.empty(np_, 3 * F, dtype=torch.float32, device=dev)
+    cols = torch.empty(3 * F, dtype=torch.float32, device=dev)
+    gamma_ = gamma.detach().float().contiguous()
+    beta_ = beta.detach().float().contiguous()
+    with _Timed("post_bwd", N * F * (2 * xhat.element_size() + dh.element_size())):
+        _lib.check(lib.sldm_post_bwd(
+            dtype_code(xhat), dout.data_ptr(), xhat.data_ptr(), rstd.data_ptr(), N, F,
+            gamma_.data_ptr(), beta_.data_ptr(), float(slope), float(drop_p),
+            seed & (2**64 - 1), _DTYPE_CODE[dh_dtype], dh.data_ptr(), partials.data_ptr(), np_,
+            _stream(dev)), "sldm_post_bwd")
+        _lib.check(lib.sldm_colsum(partials.data_ptr(), np_, 3 * F, cols.data_ptr(),
+                                   _stream(dev)), "sldm_colsum")
+    return dh, cols[:F], cols[F:2 * F], cols[2 * F:]

@@ -1,0 +1,186 @@
+"""Drop-in ``SageBlock`` (and ``SageConv``) running on hand-written gfx950 kernels.
+
+Mirrors /root/reference/src/models/blocks/sageblock.py:4-20 exactly at the API
+level — constructor ``SageBlock(hdims, dropout=None, negative_slope=None)``,
+``forward(x, edge_index)``, the module tree and therefore the state_dict keys
+
+    convs.{i}.lin_l.weight [F_{i+1}, F_i]   convs.{i}.lin_l.bias [F_{i+1}]
+    convs.{i}.lin_r.weight [F_{i+1}, F_i]   posts.{i}.0.weight / .bias [F_{i+1}]
+
+(posts.{i}.1 is LeakyReLU/ReLU, posts.{i}.2 Dropout/Identity) — so GruSage
+(grusage.py:108-110,182), MapEncoder (mapencoder.py:20-25,37), strict
+``load_state_dict`` of old snapshots (test.py:122, rcv.py:63),
+``state_dict_no_mapenc`` (grusage.py:141) and ``grads()`` (grusage.py:204)
+work unchanged.
+
+Each layer (PyG 2.7.0 SAGEConv(mean) + LayerNorm + act + Dropout) runs as
+one autograd node over the C ABI:
+  forward : gather-mean over CSR-by-dst -> [agg|x]·[W_l|W_r]^T -> bias+LN+act+dropout
+  backward: LN/act/dropout bwd -> dh·[W_l|W_r] -> dW -> 1/deg prescale ->
+            transpose gather + lin_r grad
+Dropout masks come from a counter-based hash (not torch's RNG stream), so
+parity runs use eval mode or dropout=None.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import dense, ops
+from .graph import SageGraph, get_graph
+
+
+def _act_slope(act: nn.Module) -> float:
+    if isinstance(act, nn.LeakyReLU):
+        return float(act.negative_slope)
+    if isinstance(act, nn.ReLU):
+        return 0.0
+    raise TypeError(f"SageBlock post activation must be LeakyReLU or ReLU, got {type(act)}")
+
+
+def _drop_p(drop: nn.Module) -> float:
+    if isinstance(drop, nn.Identity):
+        return 0.0
+    if isinstance(drop, nn.Dropout):
+        return float(drop.p) if drop.training else 0.0
+    raise TypeError(f"SageBlock post dropout must be Dropout or Identity, got {type(drop)}")
+
+
+def _new_seed() -> int:
+    # Drawn from torch's default CPU generator so torch.manual_seed governs it;
+    # no device sync.
+    return int(torch.randint(0, 2**62, (1,)).item())
+
+
+class _SageLayerFn(torch.autograd.Function):
+    """One SageBlock layer: SAGEConv(mean) -> LayerNorm -> act -> dropout."""
+
+    @staticmethod
+    def forward(ctx, x, wl, bl, wr, gamma, beta, graph: SageGraph, slope: float, drop_p: float,
+                seed: int, eps: float):
+        n = x.size(0)
+        agg = ops.gather_rows(x, graph.rowptr, graph.col, n, mean=True, name="gather_fwd")
+        h = dense.sage_linear_fwd(agg, x, wl, wr)
+        needs_grad = any(ctx.needs_input_grad[:6])
+        out, xhat, rstd = ops.post_fwd(h, bl, gamma, beta, eps, slope, drop_p, seed, x.dtype,
+                                       save=needs_grad)
+        if needs_grad:
+            ctx.save_for_backward(x, agg, xhat, rstd, wl, wr, gamma, beta)
+            ctx.graph = graph
+            ctx.cfg = (slope, drop_p, seed)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, agg, xhat, rstd, wl, wr, gamma, beta = ctx.saved_tensors
+        graph: SageGraph = ctx.graph
+        slope, drop_p, seed = ctx.cfg
+        dh, dgamma, dbeta, dbl = ops.post_bwd(dout, xhat, rstd, gamma, beta, slope, drop_p, seed,
+                                              dh_dtype=x.dtype)
+        d_agg, dx_r = dense.sage_linear_bwd_data(dh, wl, wr)
+        dwl, dwr = dense.sage_linear_bwd_weight(dh, agg, x)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if graph.t_rowptr is None:
+                raise RuntimeError("SageGraph was built without its transpose; rebuild with "
+                                   "transpose=True for backward")
+            ops.scale_rows_by_inv_deg_(d_agg, graph.rowptr)
+            dx = ops.gather_rows(d_agg, graph.t_rowptr, graph.t_col, x.size(0), mean=False,
+                                 addend=dx_r, name="gather_bwd")
+        return (dx, dwl.to(wl.dtype), dbl.to(wl.dtype), dwr.to(wr.dtype),
+                dgamma.to(gamma.dtype), dbeta.to(beta.dtype), None, None, None, None, None)
+
+
+class SageConv(nn.Module):
+    """Parameter layout of PyG 2.7.0 ``SAGEConv(in, out)`` with default arguments
+    (aggr='mean', root_weight=True, bias=True, normalize=False, project=False),
+    as instantiated at sageblock.py:8: ``lin_l`` (with bias) on the mean
+    aggregate, ``lin_r`` (no bias) on the root features."""
+
+    def __init__(self, in_channels: int, out_channels: int):
+        super().__init__()
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.lin_l = nn.Linear(in_channels, out_channels, bias=True)
+        self.lin_r = nn.Linear(in_channels, out_channels, bias=False)
+
+    def reset_parameters(self) -> None:
+        self.lin_l.reset_parameters()
+        self.lin_r.reset_parameters()
+
+    def forward(self, x: torch.Tensor, edge_index) -> torch.Tensor:
+        """Stand-alone conv (no post stack): lin_l(mean_j x_j) + lin_r(x)."""
+        graph = get_graph(edge_index, x.size(0), transpose=torch.is_grad_enabled())
+        agg = _MeanAggFn.apply(x, graph)
+        out = nn.functional.linear(agg.to(self.lin_l.weight.dtype), self.lin_l.weight,
+                                   self.lin_l.bias)
+        return out + nn.functional.linear(x.to(self.lin_r.weight.dtype), self.lin_r.weight)
+
+    def __repr__(self) -> str:
+        return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, aggr=mean)"
+
+
+class _MeanAggFn(torch.autograd.Function):
+    """Mean neighbour aggregation alone (PyG propagate + MeanAggregation)."""
+
+    @staticmethod
+    def forward(ctx, x, graph: SageGraph):
+        ctx.graph = graph
+        ctx.n = x.size(0)
+        return ops.gather_rows(x, graph.rowptr, graph.col, x.size(0), mean=True,
+                               name="gather_fwd")
+
+    @staticmethod
+    def backward(ctx, g):
+        graph = ctx.graph
+        g = g.contiguous().clone()
+        ops.scale_rows_by_inv_deg_(g, graph.rowptr)
+        return ops.gather_rows(g, graph.t_rowptr, graph.t_col, ctx.n, mean=False,
+                               name="gather_bwd"), None
+
+
+def sage_aggregate(x: torch.Tensor, edge_index) -> torch.Tensor:
+    """Mean aggregation over in-edges (differentiable)."""
+    graph = get_graph(edge_index, x.size(0), transpose=torch.is_grad_enabled())
+    return _MeanAggFn.apply(x, graph)
+
+
+class SageBlock(nn.Module):
+    """Drop-in for src/models/blocks/sageblock.py:4-20 (same signature, same
+    state_dict).  ``edge_index`` may also be a prebuilt :class:`SageGraph`."""
+
+    def __init__(self, hdims: list[int], dropout: float | None = None,
+                 negative_slope: float | None = None):
+        super().__init__()
+        assert len(hdims) >= 1, "hdims must contain at least one element"
+        self.convs = nn.ModuleList([SageConv(hdims[i], hdims[i + 1])
+                                    for i in range(len(hdims) - 1)])
+        self.posts = nn.ModuleList([
+            nn.Sequential(
+                nn.LayerNorm(hdims[i + 1]),
+                nn.LeakyReLU(negative_slope=negative_slope) if negative_slope is not None else nn.ReLU(),
+                nn.Dropout(p=dropout) if dropout is not None else nn.Identity(),
+            ) for i in range(len(hdims) - 1)
+        ])
+
+    def forward(self, x: torch.Tensor, edge_index) -> torch.Tensor:
+        if len(self.convs) == 0:
+            return x
+        if x.dim() != 2:
+            raise ValueError(f"SageBlock expects x [N, F], got {tuple(x.shape)}")
+        ops._require_gpu(x)
+        grad = torch.is_grad_enabled() and (
+            x.requires_grad or any(p.requires_grad for p in self.parameters()))
+        graph = get_graph(edge_index, x.size(0), transpose=grad)
+        if x.dtype not in (torch.float32, torch.bfloat16):
+            x = x.float()
+        x = x.contiguous()
+        for conv, post in zip(self.convs, self.posts):
+            ln, act, drop = post[0], post[1], post[2]
+            if not isinstance(ln, nn.LayerNorm) or ln.weight is None:
+                raise TypeError("SageBlock post[0] must be an affine LayerNorm")
+            p = _drop_p(drop)
+            x = _SageLayerFn.apply(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight,
+                                   ln.weight, ln.bias, graph, _act_slope(act), p,
+                                   _new_seed() if p > 0 else 0, float(ln.eps))
+        return x
