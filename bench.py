@@ -1,0 +1,236 @@
+"""SageBlock fwd+bwd throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4] [--no-cpu-baseline]
+
+One "step" = SageBlock.forward(x, edge_index) + backward of a fixed upstream
+gradient over one synthetic graph, dropout 0.25 in training
+mode, LeakyReLU(0.1) — the reference's training configuration (main.py:39-40).
+``value`` = E·L / t_step (layer-edges per second, whole job).  Inputs are
+resident in HBM before the timed region; the CSR is built on the first
+(warm-up) call and cached on the edge_index tensor, as for any static graph
+(``value_incl_csr_build`` re-times one step with the cache cleared).
+
+N > 1 (torchrun, one rank per GPU, RCCL): the graph's destination rows are
+partitioned across ranks (sldm_sage.dist), halo rows of x are exchanged with
+an all-gather per layer; ``scaling`` is "strong" (the graph is fixed).
+
+The JSON line also carries ``roofline`` for the dominant kernel (the CSR
+gather-mean: the SageBlock scatter-add), measured with HIP events around
+every launch on the launch stream inside the timed region, and
+``cpu_baseline``: the CPU oracle (oracle/sage_ref.py, the reference's ATen op
+sequence) timed on this host on a bounded sample (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "sldm-gnn_amd")]
+
+import torch  # noqa: E402
+
+CONFIGS = {
+    # name: (N, E, F, L, dtype, description)
+    "c1": (1_000, 5_000, 16, 2, torch.float32, "C1 1k nodes / 5k edges, F=16, 2 layers, fp32"),
+    "c2": (100_000, 1_000_000, 128, 2, torch.float32,
+           "C2 100k nodes / 1M edges, F=128, 2 layers, fp32"),
+    "c3": (1_000_000, 10_000_000, 256, 3, torch.bfloat16,
+           "C3 1M nodes / 10M edges, F=256, 3 layers, bf16"),
+    "c4": (10_000_000, 100_000_000, 256, 2, torch.bfloat16,
+           "C4 10M nodes / 100M edges, F=256, 2 layers, bf16"),
+}
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+class KernelTimer:
+    """Collects (start, end) HIP events per kernel name; durations read after sync."""
+
+    def __init__(self):
+        self.events: dict[str, list] = {}
+
+    def __call__(self, name, start, end, units):
+        self.events.setdefault(name, []).append((start, end, units))
+
+    def summary(self):
+        out = {}
+        for name, evs in self.events.items():
+            ms = [s.elapsed_time(e) for s, e, _ in evs]
+            units = [u for _, _, u in evs]
+            out[name] = dict(launches=len(ms), avg_ms=sum(ms) / len(ms),
+                             avg_bytes=sum(units) / len(units))
+        return out
+
+
+def make_graph(n, e, f, dtype, device, seed=0):
+    g = torch.Generator(device=device).manual_seed(seed)
+    src = torch.randint(0, n, (e,), generator=g, device=device)
+    dst = torch.randint(0, n, (e,), generator=g, device=device)
+    x = torch.randn(n, f, generator=g, device=device).to(dtype)
+    return torch.stack([src, dst]), x
+
+
+def cpu_baseline(cfg, threads):
+    """The oracle (plain-torch restatement of PyG SAGEConv + SageBlock, fp32) on
+    a bounded sample of the workload: same F and L, nodes and edges / 100."""
+    from oracle.sage_ref import RefSageBlock, random_graph, set_synthetic_params
+    n, e, f, L, _, _ = cfg
+    ns, es = max(n // 100, 1000), max(e // 100, 5000)
+    torch.set_num_threads(threads)
+    ei, x = random_graph(ns, es, f, seed=0)
+    blk = RefSageBlock([f] * (L + 1), dropout=0.25, negative_slope=0.1)
+    set_synthetic_params(blk, 1)
+    blk.train()
+    gout = torch.randn(ns, f, generator=torch.Generator().manual_seed(2))
+    times = []
+    t_end = time.perf_counter() + 20.0
+    for it in range(12):
+        xr = x.clone().requires_grad_(True)
+        blk.zero_grad(set_to_none=True)
+        t0 = time.perf_counter()
+        blk(xr, ei).backward(gout)
+        dt = time.perf_counter() - t0
+        if it > 0:
+            times.append(dt)
+        if time.perf_counter() > t_end and len(times) >= 3:
+            break
+    t = statistics.median(times)
+    return dict(value=es * L / t, unit="edges/s", cores=threads, kind="port",
+                sample=f"{ns} nodes / {es} edges (1/100 of the workload), F={f}, L={L}, fp32, "
+                       f"median of {len(times)} fwd+bwd after 1 warm-up; oracle/sage_ref.py",
+                ms_per_step=t * 1e3)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    from sldm_sage import SageBlock, graph_cache, ops
+
+    cfg = CONFIGS[args.config]
+    n, e, f, L, dtype, desc = cfg
+    ei, x = make_graph(n, e, f, dtype, dev)
+    torch.manual_seed(0)
+    blk = SageBlock([f] * (L + 1), dropout=0.25, negative_slope=0.1).to(dev).train()
+    gout = torch.randn(n, f, device=dev, generator=torch.Generator(device=dev).manual_seed(2)
+                       ).to(dtype)
+
+    if world > 1:
+        from sldm_sage.dist import DistSageBlock, partition_graph
+        part = partition_graph(ei, n, world, rank)
+        model = DistSageBlock(blk, part)
+        x_in = x[part.row_begin:part.row_end].contiguous()
+        g_in = gout[part.row_begin:part.row_end].contiguous()
+
+        def step():
+            xr = x_in.detach().requires_grad_(True)
+            out = model(xr)
+            out.backward(g_in)
+            return out
+    else:
+        def step():
+            xr = x.detach().requires_grad_(True)
+            out = blk(xr, ei)
+            out.backward(gout)
+            return out
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        blk.zero_grad(set_to_none=True)
+        step()
+    timer = KernelTimer()
+    barrier()
+    ops.set_timing_hook(timer)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        blk.zero_grad(set_to_none=True)
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    ops.set_timing_hook(None)
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        elapsed = tt.item()
+    kern = timer.summary()
+
+    # CSR-build-inclusive step (N=1: static-graph cache cleared once)
+    incl = None
+    if world == 1:
+        graph_cache.clear()
+        barrier()
+        t1 = time.perf_counter()
+        blk.zero_grad(set_to_none=True)
+        step()
+        barrier()
+        incl = e * L / (time.perf_counter() - t1)
+
+    ms = elapsed / args.steps * 1e3
+    value = e * L * args.steps / elapsed
+    g = kern.get("gather_fwd")
+    roof = None
+    if g:
+        achieved = g["avg_bytes"] / (g["avg_ms"] * 1e-3) / 1e9
+        roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
+                    kernel="gather_rows_kernel (forward mean aggregation)",
+                    avg_ms=round(g["avg_ms"], 4), launches=g["launches"],
+                    bytes_per_launch=int(g["avg_bytes"]))
+    kernels = {k: dict(avg_ms=round(v["avg_ms"], 4), launches=v["launches"],
+                       gbs=round(v["avg_bytes"] / (v["avg_ms"] * 1e-3) / 1e9, 1))
+               for k, v in kern.items()}
+    if rank == 0:
+        base = None
+        if world == 1 and not args.no_cpu_baseline:
+            base = cpu_baseline(cfg, args.cpu_threads)
+        line = {
+            "metric": "edges/sec SageBlock fwd+bwd",
+            "value": round(value, 1),
+            "unit": "edges/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+            "data": "synthetic (uniform random src/dst, x~N(0,1), random-init weights)",
+            "config": {"workload": desc, "nodes": n, "edges": e, "feat": f, "layers": L,
+                       "dropout": 0.25, "negative_slope": 0.1,
+                       "parallelism": f"dst-partition x{world}" if world > 1 else "single"},
+            "value_incl_csr_build": round(incl, 1) if incl else None,
+            "roofline": roof,
+            "kernels": kernels,
+            "cpu_baseline": base,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

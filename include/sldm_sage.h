@@ -87,20 +87,25 @@ int sldm_scale_rows_by_inv_deg(int dtype, void* d, int64_t ld, const int32_t* ro
  *   z    = y > 0 ? y : y * negative_slope  (ReLU: negative_slope = 0)
  *   out  = dropout(z)   keep iff u(seed, i*feat+j) >= drop_p, scale 1/(1-drop_p); drop_p in [0,1]
  * drop_p = 0 means Identity / eval mode.  xhat (out's dtype) and rstd (fp32)
- * are saved for the backward when non-NULL. */
+ * are saved for the backward when non-NULL.  The dropout key of row i is
+ * (seed, i + row_offset): a rank holding rows [r0, r1) of a partitioned graph
+ * passes row_offset = r0 and draws the single-device mask. */
 int sldm_post_fwd(int h_dtype, const void* h, int64_t ldh, int64_t num_rows, int64_t feat,
                   const float* bias, const float* gamma, const float* beta, float eps,
-                  float negative_slope, float drop_p, uint64_t seed,
+                  float negative_slope, float drop_p, uint64_t seed, int64_t row_offset,
                   int out_dtype, void* out, void* xhat, float* rstd, void* stream);
 
 /* Backward of sldm_post_fwd (autograd of Dropout, LeakyReLU/ReLU, LayerNorm):
  *   dh = rstd * (g - mean_j(g) - xhat * mean_j(g*xhat)),  g = dy*gamma
  * col_partials[p, 0:F] += dy*xhat (dgamma), [p, F:2F] dy (dbeta),
  * [p, 2F:3F] dh (d bias of lin_l), over the rows handled by partial p
- * (num_partials in [1, 4096]); reduce with sldm_colsum. */
-int sldm_post_bwd(int dtype, const void* dout, const void* xhat, const float* rstd,
+ * (num_partials in [1, 4096]); reduce with sldm_colsum.
+ * zout (the forward output, nullable) decides the activation branch
+ * (z > 0 <=> y > 0 exactly); without it y is recomputed from xhat. */
+int sldm_post_bwd(int dtype, const void* dout, const void* xhat, const void* zout,
+                  const float* rstd,
                   int64_t num_rows, int64_t feat, const float* gamma, const float* beta,
-                  float negative_slope, float drop_p, uint64_t seed,
+                  float negative_slope, float drop_p, uint64_t seed, int64_t row_offset,
                   int dh_dtype, void* dh, float* col_partials, int num_partials,
                   void* stream);
 int sldm_post_num_partials(int64_t num_rows, int64_t feat);
@@ -108,6 +113,41 @@ int sldm_post_num_partials(int64_t num_rows, int64_t feat);
 /* out[j] = sum_p partials[p*width + j], fixed order (deterministic). */
 int sldm_colsum(const float* partials, int num_partials, int64_t width, float* out,
                 void* stream);
+
+/* ----------------------------------------------------------- dense (MFMA) ---
+ * Fused forward of one layer's dense part and post stack (A6 + A7):
+ *   h   = [a0 | a1] · w^T + bias      a0 = agg [N,k0], a1 = x [N,k1],
+ *                                     w = [W_l | W_r] as [nc, k0+k1] row-major
+ *   out = dropout(act(LayerNorm(h)))  exactly as sldm_post_fwd
+ * Replaces PyG SAGEConv's lin_l(agg) + lin_r(x) (sageblock.py:18) and
+ * LayerNorm/act/Dropout (sageblock.py:11-13, :19).  nc <= 256.  xhat / rstd
+ * may be NULL (no backward).  out and xhat are [N, nc] contiguous. */
+int sldm_sage_dense_fwd(int dtype, const void* a0, int64_t lda0, int64_t k0,
+                        const void* a1, int64_t lda1, int64_t k1, const void* w,
+                        int64_t num_rows, int64_t nc, const float* bias,
+                        const float* gamma, const float* beta, float eps,
+                        float negative_slope, float drop_p, uint64_t seed, int64_t row_offset,
+                        void* out, void* xhat, float* rstd, void* stream);
+
+/* C[N, nc] = A[N, k] · B[nc, k]^T (both K-contiguous); columns j < scale_cols
+ * are divided by max(1, rowptr[i+1]-rowptr[i]) when rowptr != NULL.
+ * Backward of lin_l/lin_r w.r.t. their inputs (A8): A = dh, B = [W_l|W_r]^T,
+ * giving [dAgg/deg | dx_root] in one pass. */
+int sldm_gemm_nt_rowscale(int dtype, const void* a, int64_t lda, int64_t k,
+                          const void* b, int64_t ldb, int64_t num_rows, int64_t nc,
+                          const int32_t* rowptr, int64_t scale_cols,
+                          void* out, int64_t ldo, void* stream);
+
+/* out[mo, n0+n1] (fp32) = sum_{r < num_rows} a[r, :]^T ⊗ [b0 | b1][r, :]
+ * Weight gradients [dW_l | dW_r] = dh^T · [agg | x] (A8), split over the
+ * node dimension into fp32 slabs summed in a fixed order (deterministic).
+ * workspace: sldm_gemm_tn_workspace_bytes(num_rows, mo, n0+n1) bytes. */
+size_t sldm_gemm_tn_workspace_bytes(int64_t num_rows, int64_t mo, int64_t nn);
+int sldm_gemm_tn(int dtype, const void* a, int64_t lda, int64_t mo,
+                 const void* b0, int64_t ldb0, int64_t n0,
+                 const void* b1, int64_t ldb1, int64_t n1,
+                 int64_t num_rows, float* out, void* workspace, size_t workspace_bytes,
+                 void* stream);
 
 #ifdef __cplusplus
 }

@@ -114,13 +114,44 @@ inline int lanes_per_row(int64_t feat, int v) {
   return l;
 }
 
-// Counter-based dropout uniform in [0,1): splitmix64 finaliser of (seed, idx).
-__device__ __forceinline__ float dropout_uniform(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f);
+// Counter-based dropout: u(seed, row, col) uniform in [0,1).  One 32-bit
+// integer hash (two v_mul_lo_u32) per element on top of a per-row key, so the
+// backward regenerates the forward's mask exactly.
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t dropout_row_key(uint64_t seed, uint64_t row) {
+  return hash32((uint32_t)seed ^ hash32((uint32_t)(seed >> 32) ^ hash32((uint32_t)row) ^
+                                        (uint32_t)(row >> 32) * 0x9E3779B9u));
+}
+__device__ __forceinline__ float dropout_uniform(uint32_t row_key, uint32_t col) {
+  return (float)(hash32(row_key + col * 0x9E3779B9u) >> 8) * (1.0f / 16777216.0f);
+}
+
+// --------------------------------------------------- cross-lane reductions --
+// Sum over aligned groups of G lanes (G a power of two <= 64), result in every
+// lane of the group, bitwise identical across the group (each step adds a
+// lane pair, a+b == b+a).  DPP / swizzle steps instead of ds_bpermute chains.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float group_sum(float v, int g) {
+  if (g >= 2) v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]  (xor 1)
+  if (g >= 4) v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]  (xor 2)
+  if (g >= 8) v += dpp_f<0x141>(v);   // row_half_mirror      (quad <-> quad)
+  if (g >= 16) v += dpp_f<0x140>(v);  // row_mirror           (half <-> half)
+  if (g >= 32)                        // swap 16-lane rows inside each 32-lane half
+    v += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F));
+  if (g >= 64)
+    v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  return v;
 }
 
 }  // namespace sldm

@@ -13,17 +13,14 @@ namespace {
 
 constexpr int kBlock = 256;
 
-__device__ __forceinline__ float group_sum(float v, int lpr) {
-  for (int off = lpr >> 1; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
+using sldm::group_sum;
 
 template <typename TH, typename TO, int V, int NCH>
 __global__ __launch_bounds__(kBlock) void post_fwd_kernel(
     const TH* __restrict__ h, int64_t ldh, int64_t nrows, int feat, int lpr_log2,
     const float* __restrict__ bias, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float slope, float drop_p, float drop_scale,
-    uint64_t seed, TO* __restrict__ out, TO* __restrict__ xhat_out, float* __restrict__ rstd_out) {
+    uint64_t seed, int64_t row_off, TO* __restrict__ out, TO* __restrict__ xhat_out, float* __restrict__ rstd_out) {
   const int lpr = 1 << lpr_log2;
   const int lane_in_row = threadIdx.x & (lpr - 1);
   const int64_t row = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> lpr_log2;
@@ -61,6 +58,7 @@ __global__ __launch_bounds__(kBlock) void post_fwd_kernel(
   const float rstd = 1.0f / sqrtf(var + eps);
   if (!live) return;
   if (rstd_out && lane_in_row == 0) rstd_out[row] = rstd;
+  const uint32_t rkey = sldm::dropout_row_key(seed, (uint64_t)(row + row_off));
 
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
@@ -73,7 +71,7 @@ __global__ __launch_bounds__(kBlock) void post_fwd_kernel(
       float y = xh[k] * gamma[f] + beta[f];
       float a = y > 0.0f ? y : y * slope;
       if (drop_p > 0.0f) {
-        float u = sldm::dropout_uniform(seed, (uint64_t)row * (uint64_t)feat + (uint64_t)f);
+        float u = sldm::dropout_uniform(rkey, (uint32_t)f);
         a = (u >= drop_p) ? a * drop_scale : 0.0f;
       }
       z[k] = a;
@@ -88,9 +86,10 @@ __global__ __launch_bounds__(kBlock) void post_fwd_kernel(
 // groups in LDS and written as partials[blockIdx.x][3][feat].
 template <typename T, typename TD, int V, int NCH>
 __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
-    const T* __restrict__ dout, const T* __restrict__ xhat, const float* __restrict__ rstd,
+    const T* __restrict__ dout, const T* __restrict__ xhat, const T* __restrict__ zout,
+    const float* __restrict__ rstd,
     int64_t nrows, int feat, int lpr_log2, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float slope, float drop_p, float drop_scale, uint64_t seed,
+    const float* __restrict__ beta, float slope, float drop_p, float drop_scale, uint64_t seed, int64_t row_off,
     TD* __restrict__ dh, float* __restrict__ partials) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [kBlock/lpr][3][feat] reused
   const int lpr = 1 << lpr_log2;
@@ -120,24 +119,31 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
     const bool live = row < nrows;
     const int64_t r = live ? row : 0;
     const float rs = rstd[r];
+    const uint32_t rkey = sldm::dropout_row_key(seed, (uint64_t)(r + row_off));
     float xh[NCH][V], gx[NCH][V], dy[NCH][V];
     float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      float go[V];
+      float go[V], zo[V];
       sldm::Vec<T, V>::load(dout + r * (int64_t)feat + f0[c], go);
       sldm::Vec<T, V>::load(xhat + r * (int64_t)feat + f0[c], xh[c]);
+      if (zout) sldm::Vec<T, V>::load(zout + r * (int64_t)feat + f0[c], zo);
 #pragma unroll
       for (int k = 0; k < V; ++k) {
         const int f = f0[c] + k;
         const float g = gamma[f];
-        const float y = xh[c][k] * g + beta[f];
         float d = go[k];
+        bool keep = true;
         if (drop_p > 0.0f) {
-          float u = sldm::dropout_uniform(seed, (uint64_t)r * (uint64_t)feat + (uint64_t)f);
-          d = (u >= drop_p) ? d * drop_scale : 0.0f;
+          float u = sldm::dropout_uniform(rkey, (uint32_t)f);
+          keep = u >= drop_p;
+          d = keep ? d * drop_scale : 0.0f;
         }
-        d = y > 0.0f ? d : d * slope;
+        // Activation branch: from the saved output when given (sign(z) ==
+        // sign(y) exactly, even with bf16 storage); else from y = xhat*g+b,
+        // which a rounded xhat can flip where |y| is tiny.
+        const bool pos = zout ? (keep ? zo[k] > 0.0f : true) : (xh[c][k] * g + beta[f] > 0.0f);
+        d = pos ? d : d * slope;
         if (!act[c] || !live) { d = 0.0f; xh[c][k] = 0.0f; }
         dy[c][k] = d;
         gx[c][k] = d * g;
@@ -210,14 +216,14 @@ RowGeom row_geom(int elem_bytes, int64_t feat, std::initializer_list<const void*
 template <typename TH, typename TO, int V>
 int post_fwd_nch(const RowGeom& g, const void* h, int64_t ldh, int64_t nrows, int feat,
                  const float* bias, const float* gamma, const float* beta, float eps,
-                 float slope, float p, float scale, uint64_t seed, void* out, void* xhat,
+                 float slope, float p, float scale, uint64_t seed, int64_t row_off, void* out, void* xhat,
                  float* rstd, hipStream_t stream) {
   const int64_t grid = ((nrows << g.lpr_log2) + kBlock - 1) / kBlock;
 #define SLDM_PF_CASE(NC)                                                                     \
   case NC:                                                                                   \
     post_fwd_kernel<TH, TO, V, NC><<<(unsigned)grid, kBlock, 0, stream>>>(                   \
         reinterpret_cast<const TH*>(h), ldh, nrows, feat, g.lpr_log2, bias, gamma, beta,     \
-        eps, slope, p, scale, seed, reinterpret_cast<TO*>(out), reinterpret_cast<TO*>(xhat), \
+        eps, slope, p, scale, seed, row_off, reinterpret_cast<TO*>(out), reinterpret_cast<TO*>(xhat), \
         rstd);                                                                               \
     break;
   switch (g.nch) {
@@ -234,9 +240,9 @@ int post_fwd_nch(const RowGeom& g, const void* h, int64_t ldh, int64_t nrows, in
 }
 
 template <typename T, typename TD, int V>
-int post_bwd_nch(const RowGeom& g, const void* dout, const void* xhat, const float* rstd,
+int post_bwd_nch(const RowGeom& g, const void* dout, const void* xhat, const void* zout, const float* rstd,
                  int64_t nrows, int feat, const float* gamma, const float* beta, float slope,
-                 float p, float scale, uint64_t seed, void* dh, float* partials, int np,
+                 float p, float scale, uint64_t seed, int64_t row_off, void* dh, float* partials, int np,
                  hipStream_t stream) {
   const size_t lds = sizeof(float) * 3 * (size_t)feat * (kBlock >> g.lpr_log2);
   if (lds > 160 * 1024) {
@@ -246,8 +252,8 @@ int post_bwd_nch(const RowGeom& g, const void* dout, const void* xhat, const flo
 #define SLDM_PB_CASE(NC)                                                                       \
   case NC:                                                                                     \
     post_bwd_kernel<T, TD, V, NC><<<np, kBlock, lds, stream>>>(                                \
-        reinterpret_cast<const T*>(dout), reinterpret_cast<const T*>(xhat), rstd, nrows, feat, \
-        g.lpr_log2, gamma, beta, slope, p, scale, seed, reinterpret_cast<TD*>(dh), partials);  \
+        reinterpret_cast<const T*>(dout), reinterpret_cast<const T*>(xhat), reinterpret_cast<const T*>(zout), rstd, nrows, feat, \
+        g.lpr_log2, gamma, beta, slope, p, scale, seed, row_off, reinterpret_cast<TD*>(dh), partials);  \
     break;
   switch (g.nch) {
     SLDM_PB_CASE(1)
@@ -265,40 +271,40 @@ int post_bwd_nch(const RowGeom& g, const void* dout, const void* xhat, const flo
 template <typename TH, typename TO>
 int post_fwd_t(const RowGeom& g, const void* h, int64_t ldh, int64_t nrows, int feat,
                const float* bias, const float* gamma, const float* beta, float eps, float slope,
-               float p, float scale, uint64_t seed, void* out, void* xhat, float* rstd,
+               float p, float scale, uint64_t seed, int64_t row_off, void* out, void* xhat, float* rstd,
                hipStream_t stream) {
   switch (g.v) {
     case 8:
       if constexpr (sizeof(TH) == 2 && sizeof(TO) == 2)
-        return post_fwd_nch<TH, TO, 8>(g, h, ldh, nrows, feat, bias, gamma, beta, eps, slope, p, scale, seed, out, xhat, rstd, stream);
+        return post_fwd_nch<TH, TO, 8>(g, h, ldh, nrows, feat, bias, gamma, beta, eps, slope, p, scale, seed, row_off, out, xhat, rstd, stream);
       break;
     case 4:
-      return post_fwd_nch<TH, TO, 4>(g, h, ldh, nrows, feat, bias, gamma, beta, eps, slope, p, scale, seed, out, xhat, rstd, stream);
+      return post_fwd_nch<TH, TO, 4>(g, h, ldh, nrows, feat, bias, gamma, beta, eps, slope, p, scale, seed, row_off, out, xhat, rstd, stream);
     case 2:
-      return post_fwd_nch<TH, TO, 2>(g, h, ldh, nrows, feat, bias, gamma, beta, eps, slope, p, scale, seed, out, xhat, rstd, stream);
+      return post_fwd_nch<TH, TO, 2>(g, h, ldh, nrows, feat, bias, gamma, beta, eps, slope, p, scale, seed, row_off, out, xhat, rstd, stream);
     case 1:
-      return post_fwd_nch<TH, TO, 1>(g, h, ldh, nrows, feat, bias, gamma, beta, eps, slope, p, scale, seed, out, xhat, rstd, stream);
+      return post_fwd_nch<TH, TO, 1>(g, h, ldh, nrows, feat, bias, gamma, beta, eps, slope, p, scale, seed, row_off, out, xhat, rstd, stream);
   }
   sldm::set_error("sldm_post_fwd: vector width %d", g.v);
   return SLDM_ERR_ARG;
 }
 
 template <typename T, typename TD>
-int post_bwd_t(const RowGeom& g, const void* dout, const void* xhat, const float* rstd,
+int post_bwd_t(const RowGeom& g, const void* dout, const void* xhat, const void* zout, const float* rstd,
                int64_t nrows, int feat, const float* gamma, const float* beta, float slope,
-               float p, float scale, uint64_t seed, void* dh, float* partials, int np,
+               float p, float scale, uint64_t seed, int64_t row_off, void* dh, float* partials, int np,
                hipStream_t stream) {
   switch (g.v) {
     case 8:
       if constexpr (sizeof(T) == 2 && sizeof(TD) == 2)
-        return post_bwd_nch<T, TD, 8>(g, dout, xhat, rstd, nrows, feat, gamma, beta, slope, p, scale, seed, dh, partials, np, stream);
+        return post_bwd_nch<T, TD, 8>(g, dout, xhat, zout, rstd, nrows, feat, gamma, beta, slope, p, scale, seed, row_off, dh, partials, np, stream);
       break;
     case 4:
-      return post_bwd_nch<T, TD, 4>(g, dout, xhat, rstd, nrows, feat, gamma, beta, slope, p, scale, seed, dh, partials, np, stream);
+      return post_bwd_nch<T, TD, 4>(g, dout, xhat, zout, rstd, nrows, feat, gamma, beta, slope, p, scale, seed, row_off, dh, partials, np, stream);
     case 2:
-      return post_bwd_nch<T, TD, 2>(g, dout, xhat, rstd, nrows, feat, gamma, beta, slope, p, scale, seed, dh, partials, np, stream);
+      return post_bwd_nch<T, TD, 2>(g, dout, xhat, zout, rstd, nrows, feat, gamma, beta, slope, p, scale, seed, row_off, dh, partials, np, stream);
     case 1:
-      return post_bwd_nch<T, TD, 1>(g, dout, xhat, rstd, nrows, feat, gamma, beta, slope, p, scale, seed, dh, partials, np, stream);
+      return post_bwd_nch<T, TD, 1>(g, dout, xhat, zout, rstd, nrows, feat, gamma, beta, slope, p, scale, seed, row_off, dh, partials, np, stream);
   }
   sldm::set_error("sldm_post_bwd: vector width %d", g.v);
   return SLDM_ERR_ARG;
@@ -309,7 +315,7 @@ int post_bwd_t(const RowGeom& g, const void* dout, const void* xhat, const float
 extern "C" int sldm_post_fwd(int h_dtype, const void* h, int64_t ldh, int64_t num_rows,
                              int64_t feat, const float* bias, const float* gamma,
                              const float* beta, float eps, float negative_slope, float drop_p,
-                             uint64_t seed, int out_dtype, void* out, void* xhat, float* rstd,
+                             uint64_t seed, int64_t row_off, int out_dtype, void* out, void* xhat, float* rstd,
                              void* stream_) {
   SLDM_REQUIRE(num_rows >= 0 && feat > 0 && feat <= 4096, "sldm_post_fwd: bad sizes");
   if (num_rows == 0) return SLDM_OK;
@@ -327,11 +333,11 @@ extern "C" int sldm_post_fwd(int h_dtype, const void* h, int64_t ldh, int64_t nu
   }
   SLDM_REQUIRE(ldh % g.v == 0, "sldm_post_fwd: ldh not aligned");
   if (h_dtype == SLDM_F32 && out_dtype == SLDM_F32)
-    return post_fwd_t<float, float>(g, h, ldh, num_rows, f, bias, gamma, beta, eps, negative_slope, drop_p, scale, seed, out, xhat, rstd, stream);
+    return post_fwd_t<float, float>(g, h, ldh, num_rows, f, bias, gamma, beta, eps, negative_slope, drop_p, scale, seed, row_off, out, xhat, rstd, stream);
   if (h_dtype == SLDM_BF16 && out_dtype == SLDM_BF16)
-    return post_fwd_t<uint16_t, uint16_t>(g, h, ldh, num_rows, f, bias, gamma, beta, eps, negative_slope, drop_p, scale, seed, out, xhat, rstd, stream);
+    return post_fwd_t<uint16_t, uint16_t>(g, h, ldh, num_rows, f, bias, gamma, beta, eps, negative_slope, drop_p, scale, seed, row_off, out, xhat, rstd, stream);
   if (h_dtype == SLDM_F32 && out_dtype == SLDM_BF16)
-    return post_fwd_t<float, uint16_t>(g, h, ldh, num_rows, f, bias, gamma, beta, eps, negative_slope, drop_p, scale, seed, out, xhat, rstd, stream);
+    return post_fwd_t<float, uint16_t>(g, h, ldh, num_rows, f, bias, gamma, beta, eps, negative_slope, drop_p, scale, seed, row_off, out, xhat, rstd, stream);
   sldm::set_error("sldm_post_fwd: dtype pair (%d -> %d) unsupported", h_dtype, out_dtype);
   return SLDM_ERR_ARG;
 }
@@ -345,10 +351,10 @@ extern "C" int sldm_post_num_partials(int64_t num_rows, int64_t feat) {
   return (int)(np < 1 ? 1 : np);
 }
 
-extern "C" int sldm_post_bwd(int dtype, const void* dout, const void* xhat, const float* rstd,
+extern "C" int sldm_post_bwd(int dtype, const void* dout, const void* xhat, const void* zout, const float* rstd,
                              int64_t num_rows, int64_t feat, const float* gamma,
                              const float* beta, float negative_slope, float drop_p,
-                             uint64_t seed, int dh_dtype, void* dh, float* col_partials,
+                             uint64_t seed, int64_t row_off, int dh_dtype, void* dh, float* col_partials,
                              int num_partials, void* stream_) {
   SLDM_REQUIRE(feat > 0 && feat <= 4096 && num_rows >= 0, "sldm_post_bwd: bad sizes");
   SLDM_REQUIRE(num_partials >= 1 && num_partials <= 4096, "sldm_post_bwd: num_partials=%d",
@@ -363,11 +369,11 @@ extern "C" int sldm_post_bwd(int dtype, const void* dout, const void* xhat, cons
   int eb = (dtype == SLDM_F32 || dh_dtype == SLDM_F32) ? 4 : 2;
   RowGeom g = row_geom(eb, feat, {dout, xhat, dh});
   if (dtype == SLDM_F32 && dh_dtype == SLDM_F32)
-    return post_bwd_t<float, float>(g, dout, xhat, rstd, num_rows, f, gamma, beta, negative_slope, drop_p, scale, seed, dh, col_partials, num_partials, stream);
+    return post_bwd_t<float, float>(g, dout, xhat, zout, rstd, num_rows, f, gamma, beta, negative_slope, drop_p, scale, seed, row_off, dh, col_partials, num_partials, stream);
   if (dtype == SLDM_BF16 && dh_dtype == SLDM_BF16)
-    return post_bwd_t<uint16_t, uint16_t>(g, dout, xhat, rstd, num_rows, f, gamma, beta, negative_slope, drop_p, scale, seed, dh, col_partials, num_partials, stream);
+    return post_bwd_t<uint16_t, uint16_t>(g, dout, xhat, zout, rstd, num_rows, f, gamma, beta, negative_slope, drop_p, scale, seed, row_off, dh, col_partials, num_partials, stream);
   if (dtype == SLDM_BF16 && dh_dtype == SLDM_F32)
-    return post_bwd_t<uint16_t, float>(g, dout, xhat, rstd, num_rows, f, gamma, beta, negative_slope, drop_p, scale, seed, dh, col_partials, num_partials, stream);
+    return post_bwd_t<uint16_t, float>(g, dout, xhat, zout, rstd, num_rows, f, gamma, beta, negative_slope, drop_p, scale, seed, row_off, dh, col_partials, num_partials, stream);
   sldm::set_error("sldm_post_bwd: dtype pair (%d, dh %d) unsupported", dtype, dh_dtype);
   return SLDM_ERR_ARG;
 }

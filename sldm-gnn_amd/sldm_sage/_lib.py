@@ -36,12 +36,22 @@ _SIGNATURES = {
                                                   _c_i64, _vp]),
     "sldm_post_fwd": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp,
                                      ctypes.c_float, ctypes.c_float, ctypes.c_float,
-                                     ctypes.c_uint64, ctypes.c_int, _vp, _vp, _vp, _vp]),
-    "sldm_post_bwd": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp,
-                                     ctypes.c_float, ctypes.c_float, ctypes.c_uint64,
+                                     ctypes.c_uint64, _c_i64, ctypes.c_int, _vp, _vp, _vp, _vp]),
+    "sldm_post_bwd": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp,
+                                     ctypes.c_float, ctypes.c_float, ctypes.c_uint64, _c_i64,
                                      ctypes.c_int, _vp, _vp, ctypes.c_int, _vp]),
     "sldm_post_num_partials": (ctypes.c_int, [_c_i64, _c_i64]),
     "sldm_colsum": (ctypes.c_int, [_vp, ctypes.c_int, _c_i64, _vp, _vp]),
+    "sldm_sage_dense_fwd": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _c_i64, _vp, _c_i64,
+                                           _c_i64, _vp, _c_i64, _c_i64, _vp, _vp, _vp,
+                                           ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                           ctypes.c_uint64, _c_i64, _vp, _vp, _vp, _vp]),
+    "sldm_gemm_nt_rowscale": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _c_i64, _vp, _c_i64,
+                                             _c_i64, _c_i64, _vp, _c_i64, _vp, _c_i64, _vp]),
+    "sldm_gemm_tn_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, _c_i64]),
+    "sldm_gemm_tn": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64,
+                                    _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, ctypes.c_size_t,
+                                    _vp]),
 }
 
 _lock = threading.Lock()

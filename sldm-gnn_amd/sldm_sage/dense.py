@@ -1,31 +1,41 @@
-"""The dense part of a SAGEConv layer: one contraction
-[agg | x] · [W_l | W_r]^T per layer, and its two backward contractions.
-
-Interim implementation: PyTorch GEMMs (hipBLASLt on ROCm) in the layer's
-storage dtype.  The hand-written MFMA kernels replace these functions.
+"""The dense part of a SAGEConv layer on hand-written MFMA
+kernels: one contraction [agg | x] · [W_l | W_r]^T per layer with the bias,
+LayerNorm, activation and dropout fused in its epilogue, and the two backward
+contractions (input grads with the 1/deg prescale fused; weight grads split
+over the node dimension).
 """
 from __future__ import annotations
 
 import torch
 
-
-def sage_linear_fwd(agg: torch.Tensor, x: torch.Tensor, wl: torch.Tensor,
-                    wr: torch.Tensor) -> torch.Tensor:
-    """h = agg · W_l^T + x · W_r^T   (bias is added in the post kernel)."""
-    dt = x.dtype
-    h = torch.mm(agg, wl.to(dt).t())
-    h.addmm_(x, wr.to(dt).t())
-    return h
+from . import ops
 
 
-def sage_linear_bwd_data(dh: torch.Tensor, wl: torch.Tensor, wr: torch.Tensor):
-    """(d_agg, dx_root) = (dh · W_l, dh · W_r)."""
-    dt = dh.dtype
-    return torch.mm(dh, wl.to(dt)), torch.mm(dh, wr.to(dt))
+def weight_cat(wl: torch.Tensor, wr: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """[W_l | W_r] as [F_out, 2 F_in] in the compute dtype (parameter plumbing)."""
+    return torch.cat([wl.detach(), wr.detach()], dim=1).to(dtype).contiguous()
+
+
+def sage_layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p, seed, save,
+                   row_offset=0):
+    """out = dropout(act(LN(agg·W_l^T + b_l + x·W_r^T)))  -> (out, xhat, rstd)."""
+    wcat = weight_cat(wl, wr, x.dtype)
+    return ops.sage_dense_fwd(agg, x, wcat, bl, gamma, beta, eps, slope, drop_p, seed, save,
+                              row_offset)
+
+
+def sage_linear_bwd_data(dh: torch.Tensor, wl: torch.Tensor, wr: torch.Tensor,
+                         rowptr: torch.Tensor):
+    """[dAgg / deg | dx_root] = dh · [W_l | W_r] as one [N, 2 F_in] buffer; returns
+    the two column views (prescaled aggregate grad, root-path grad)."""
+    fi = wl.size(1)
+    wcat_t = weight_cat(wl, wr, dh.dtype).t().contiguous()     # [2 F_in, F_out]
+    buf = ops.gemm_nt_rowscale(dh, wcat_t, rowptr, scale_cols=fi)
+    return buf[:, :fi], buf[:, fi:]
 
 
 def sage_linear_bwd_weight(dh: torch.Tensor, agg: torch.Tensor, x: torch.Tensor):
     """(dW_l, dW_r) = (dh^T · agg, dh^T · x), fp32."""
-    if dh.dtype == torch.float32:
-        return torch.mm(dh.t(), agg), torch.mm(dh.t(), x)
-    return torch.mm(dh.t(), agg).float(), torch.mm(dh.t(), x).float()
+    fi = x.size(1)
+    dw = ops.gemm_tn(dh, agg, x)
+    return dw[:, :fi].contiguous(), dw[:, fi:].contiguous()

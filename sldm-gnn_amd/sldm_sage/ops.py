@@ -146,9 +146,71 @@ def scale_rows_by_inv_deg_(d: torch.Tensor, rowptr: torch.Tensor) -> torch.Tenso
     return d
 
 
+# ------------------------------------------------------------ dense (MFMA) --
+def sage_dense_fwd(agg: torch.Tensor, x: torch.Tensor, wcat: torch.Tensor, bias, gamma, beta,
+                   eps: float, slope: float, drop_p: float, seed: int, save: bool,
+                   row_offset: int = 0):
+    """out = dropout(act(LN([agg|x]·wcat^T + bias))); returns (out, xhat|None, rstd|None).
+
+    wcat is [F_out, 2 F_in] (= [W_l | W_r]) in x's dtype."""
+    dev = _require_gpu(agg, x, wcat, gamma, beta, bias)
+    n, fi = x.shape
+    fo = wcat.size(0)
+    assert agg.shape == x.shape and agg.stride(1) == 1 and x.stride(1) == 1
+    assert wcat.is_contiguous() and wcat.shape == (fo, 2 * fi) and wcat.dtype == x.dtype
+    out = torch.empty(n, fo, dtype=x.dtype, device=dev)
+    xhat = torch.empty(n, fo, dtype=x.dtype, device=dev) if save else None
+    rstd = torch.empty(n, dtype=torch.float32, device=dev) if save else None
+    f32 = lambda t: None if t is None else t.detach().float().contiguous()  # noqa: E731
+    bias_, gamma_, beta_ = f32(bias), f32(gamma), f32(beta)
+    s = x.element_size()
+    with _Timed("dense_fwd", (2 * n * fi + n * fo * (2 if save else 1)) * s):
+        _lib.check(_lib.load().sldm_sage_dense_fwd(
+            dtype_code(x), agg.data_ptr(), agg.stride(0), fi, x.data_ptr(), x.stride(0), fi,
+            wcat.data_ptr(), n, fo, _ptr(bias_), gamma_.data_ptr(), beta_.data_ptr(), float(eps),
+            float(slope), float(drop_p), seed & (2**64 - 1), int(row_offset), out.data_ptr(), _ptr(xhat),
+            _ptr(rstd), _stream(dev)), "sldm_sage_dense_fwd")
+    return out, xhat, rstd
+
+
+def gemm_nt_rowscale(a: torch.Tensor, b: torch.Tensor, rowptr: torch.Tensor | None,
+                     scale_cols: int) -> torch.Tensor:
+    """C = a · b^T, columns < scale_cols divided by max(1, deg(row))."""
+    dev = _require_gpu(a, b, rowptr)
+    assert a.stride(1) == 1 and b.is_contiguous() and a.dtype == b.dtype
+    n, k = a.shape
+    nc = b.size(0)
+    out = torch.empty(n, nc, dtype=a.dtype, device=dev)
+    with _Timed("dense_bwd_data", (n * k + n * nc) * a.element_size()):
+        _lib.check(_lib.load().sldm_gemm_nt_rowscale(
+            dtype_code(a), a.data_ptr(), a.stride(0), k, b.data_ptr(), b.stride(0), n, nc,
+            _ptr(rowptr), scale_cols, out.data_ptr(), out.stride(0), _stream(dev)),
+            "sldm_gemm_nt_rowscale")
+    return out
+
+
+def gemm_tn(a: torch.Tensor, b0: torch.Tensor, b1: torch.Tensor | None) -> torch.Tensor:
+    """fp32 [a.size(1), b0.size(1)+b1.size(1)] = a^T · [b0 | b1] (sum over rows)."""
+    dev = _require_gpu(a, b0, b1)
+    assert a.stride(1) == 1 and b0.stride(1) == 1 and (b1 is None or b1.stride(1) == 1)
+    rows, mo = a.shape
+    n0 = b0.size(1)
+    n1 = 0 if b1 is None else b1.size(1)
+    lib = _lib.load()
+    out = torch.empty(mo, n0 + n1, dtype=torch.float32, device=dev)
+    ws_bytes = lib.sldm_gemm_tn_workspace_bytes(rows, mo, n0 + n1)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    with _Timed("dense_bwd_weight", rows * (mo + n0 + n1) * a.element_size()):
+        _lib.check(lib.sldm_gemm_tn(
+            dtype_code(a), a.data_ptr(), a.stride(0), mo, b0.data_ptr(), b0.stride(0), n0,
+            _ptr(b1), b1.stride(0) if b1 is not None else 0, n1, rows, out.data_ptr(),
+            ws.data_ptr(), ws_bytes, _stream(dev)), "sldm_gemm_tn")
+    return out
+
+
 # ------------------------------------------------------------------- post --
 def post_fwd(h: torch.Tensor, bias, gamma, beta, eps: float, slope: float, drop_p: float,
-             seed: int, out_dtype: torch.dtype, save: bool):
+             seed: int, out_dtype: torch.dtype, save: bool, row_offset: int = 0):
     """bias + LayerNorm + (Leaky)ReLU + dropout; returns (out, xhat|None, rstd|None)."""
     dev = _require_gpu(h, gamma, beta, bias)
     N, F = h.shape
@@ -162,19 +224,24 @@ def post_fwd(h: torch.Tensor, bias, gamma, beta, eps: float, slope: float, drop_
     with _Timed("post_fwd", N * F * (h.element_size() + out.element_size() * (2 if save else 1))):
         _lib.check(_lib.load().sldm_post_fwd(
             dtype_code(h), h.data_ptr(), h.stride(0), N, F, _ptr(bias_), gamma_.data_ptr(),
-            beta_.data_ptr(), float(eps), float(slope), float(drop_p), seed & (2**64 - 1),
+            beta_.data_ptr(), float(eps), float(slope), float(drop_p), seed & (2**64 - 1), int(row_offset),
             _DTYPE_CODE[out_dtype], out.data_ptr(), _ptr(xhat), _ptr(rstd), _stream(dev)),
             "sldm_post_fwd")
     return out, xhat, rstd
 
 
 def post_bwd(dout: torch.Tensor, xhat: torch.Tensor, rstd: torch.Tensor, gamma, beta,
-             slope: float, drop_p: float, seed: int, dh_dtype: torch.dtype):
-    """Returns (dh [N,F], dgamma [F], dbeta [F], dbias [F]) (the last three fp32)."""
-    dev = _require_gpu(dout, xhat, rstd)
+             slope: float, drop_p: float, seed: int, dh_dtype: torch.dtype,
+             zout: torch.Tensor | None = None, row_offset: int = 0):
+    """Returns (dh [N,F], dgamma [F], dbeta [F], dbias [F]) (the last three fp32).
+
+    ``zout`` (the forward output) fixes the activation branch exactly."""
+    dev = _require_gpu(dout, xhat, rstd, zout)
     N, F = xhat.shape
     if dout.dtype != xhat.dtype or dout.stride(1) != 1 or dout.stride(0) != F:
         dout = dout.to(xhat.dtype).contiguous()
+    if zout is not None:
+        assert zout.dtype == xhat.dtype and zout.is_contiguous() and zout.shape == xhat.shape
     lib = _lib.load()
     np_ = lib.sldm_post_num_partials(N, F)
     dh = torch.empty(N, F, dtype=dh_dtype, device=dev)
@@ -184,9 +251,9 @@ def post_bwd(dout: torch.Tensor, xhat: torch.Tensor, rstd: torch.Tensor, gamma, 
     beta_ = beta.detach().float().contiguous()
     with _Timed("post_bwd", N * F * (2 * xhat.element_size() + dh.element_size())):
         _lib.check(lib.sldm_post_bwd(
-            dtype_code(xhat), dout.data_ptr(), xhat.data_ptr(), rstd.data_ptr(), N, F,
+            dtype_code(xhat), dout.data_ptr(), xhat.data_ptr(), _ptr(zout), rstd.data_ptr(), N, F,
             gamma_.data_ptr(), beta_.data_ptr(), float(slope), float(drop_p),
-            seed & (2**64 - 1), _DTYPE_CODE[dh_dtype], dh.data_ptr(), partials.data_ptr(), np_,
+            seed & (2**64 - 1), int(row_offset), _DTYPE_CODE[dh_dtype], dh.data_ptr(), partials.data_ptr(), np_,
             _stream(dev)), "sldm_post_bwd")
         _lib.check(lib.sldm_colsum(partials.data_ptr(), np_, 3 * F, cols.data_ptr(),
                                    _stream(dev)), "sldm_colsum")

@@ -60,32 +60,34 @@ class _SageLayerFn(torch.autograd.Function):
                 seed: int, eps: float):
         n = x.size(0)
         agg = ops.gather_rows(x, graph.rowptr, graph.col, n, mean=True, name="gather_fwd")
-        h = dense.sage_linear_fwd(agg, x, wl, wr)
         needs_grad = any(ctx.needs_input_grad[:6])
-        out, xhat, rstd = ops.post_fwd(h, bl, gamma, beta, eps, slope, drop_p, seed, x.dtype,
-                                       save=needs_grad)
+        out, xhat, rstd = dense.sage_layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope,
+                                               drop_p, seed, save=needs_grad)
         if needs_grad:
-            ctx.save_for_backward(x, agg, xhat, rstd, wl, wr, gamma, beta)
+            # `out` is saved too (it is the next layer's input anyway): its sign
+            # fixes the activation branch exactly in the backward.
+            ctx.save_for_backward(x, agg, xhat, rstd, wl, wr, gamma, beta, out)
             ctx.graph = graph
             ctx.cfg = (slope, drop_p, seed)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, agg, xhat, rstd, wl, wr, gamma, beta = ctx.saved_tensors
+        x, agg, xhat, rstd, wl, wr, gamma, beta, out = ctx.saved_tensors
         graph: SageGraph = ctx.graph
         slope, drop_p, seed = ctx.cfg
         dh, dgamma, dbeta, dbl = ops.post_bwd(dout, xhat, rstd, gamma, beta, slope, drop_p, seed,
-                                              dh_dtype=x.dtype)
-        d_agg, dx_r = dense.sage_linear_bwd_data(dh, wl, wr)
+                                              dh_dtype=x.dtype, zout=out)
         dwl, dwr = dense.sage_linear_bwd_weight(dh, agg, x)
         dx = None
         if ctx.needs_input_grad[0]:
             if graph.t_rowptr is None:
                 raise RuntimeError("SageGraph was built without its transpose; rebuild with "
                                    "transpose=True for backward")
-            ops.scale_rows_by_inv_deg_(d_agg, graph.rowptr)
-            dx = ops.gather_rows(d_agg, graph.t_rowptr, graph.t_col, x.size(0), mean=False,
+            # [dAgg/deg | dx_root] in one MFMA pass, then the transpose gather
+            # adds the root-path gradient as it sums over out-edges.
+            g, dx_r = dense.sage_linear_bwd_data(dh, wl, wr, graph.rowptr)
+            dx = ops.gather_rows(g, graph.t_rowptr, graph.t_col, x.size(0), mean=False,
                                  addend=dx_r, name="gather_bwd")
         return (dx, dwl.to(wl.dtype), dbl.to(wl.dtype), dwr.to(wr.dtype),
                 dgamma.to(gamma.dtype), dbeta.to(beta.dtype), None, None, None, None, None)

@@ -1,0 +1,81 @@
+"""Multi-rank protocol of sldm_sage.dist over gloo on CPU (world sizes 2 and 3).
+
+Each rank runs DistSageBlock on its destination-row partition (per-rank
+compute from the test's plain-torch backend) and must reproduce the oracle's
+full-graph output rows, input-gradient rows and the full parameter gradients.
+"""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, hdims, n, e, q):
+    sys.path[:0] = [HERE, os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "sldm-gnn_amd")]
+    import torch.distributed as dist
+
+    from _cpu_backend import CpuBackend
+    from _helpers import oracle_block, run_oracle
+    from oracle.sage_ref import random_graph
+    from sldm_sage import SageBlock
+    from sldm_sage.dist import DistSageBlock, partition_graph
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        ei, x = random_graph(n, e, hdims[0], seed=3)
+        gout = torch.randn(n, hdims[-1], generator=torch.Generator().manual_seed(4))
+        ref = oracle_block(hdims, 0.1)
+        out_r, dx_r, grads_r = run_oracle(ref, x, ei, gout)
+
+        blk = SageBlock(hdims, None, 0.1)
+        if rank == 0:
+            blk.load_state_dict(ref.state_dict())   # other ranks get it by broadcast
+        part = partition_graph(ei, n, world, rank, backend=CpuBackend)
+        model = DistSageBlock(blk, part, backend=CpuBackend)
+        r0, r1 = part.row_begin, part.row_end
+        xl = x[r0:r1].clone().requires_grad_(True)
+        out = model(xl)
+        out.backward(gout[r0:r1])
+        tol = dict(atol=1e-5, rtol=1e-5)
+        torch.testing.assert_close(out.detach(), out_r[r0:r1], **tol)
+        torch.testing.assert_close(xl.grad, dx_r[r0:r1], **tol)
+        for k, p in blk.named_parameters():
+            torch.testing.assert_close(p.grad, grads_r[k], atol=1e-4, rtol=1e-4)
+        q.put((rank, "ok"))
+    except Exception as exc:  # report to the parent
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        raise exc
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 300), (3, 301)])
+def test_dist_sageblock_matches_single_device(world, n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, [8, 12, 8], n, 6 * n, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, msg in results:
+        assert msg == "ok", f"rank {rank}:\n{msg}"
