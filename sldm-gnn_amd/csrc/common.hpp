@@ -154,6 +154,21 @@ __device__ __forceinline__ float group_sum(float v, int g) {
   return v;
 }
 
+// Big-tile bf16 dense kernels (gemm_big.hip); the gemm.hip entry points route
+// conforming shapes to them.  SLDM_BIG_GEMM=0 in the environment disables them
+// (A/B comparisons against the 64-row kernels).
+bool big_gemm_enabled();
+bool big_gemm_ok(int64_t k0, int64_t K, int64_t bn, const void* a0, int64_t lda0,
+                 const void* a1, int64_t lda1, const void* b, int64_t ldb, int64_t ldo);
+int big_dense_fwd(const void* a0, int64_t lda0, int64_t k0, const void* a1, int64_t lda1,
+                  int64_t k1, const void* w, int64_t num_rows, int64_t nc, const float* bias,
+                  const float* gamma, const float* beta, float eps, float slope, float drop_p,
+                  uint64_t seed, int64_t row_off, void* out, void* xhat, float* rstd,
+                  hipStream_t stream);
+int big_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int64_t ldb,
+                      int64_t num_rows, int64_t nc, int64_t bn, const int32_t* rowptr,
+                      int64_t scale_cols, void* out, int64_t ldo, hipStream_t stream);
+
 }  // namespace sldm
 
 #define SLDM_REQUIRE(cond, ...)          \
