@@ -194,8 +194,16 @@ def main():
     roof = None
     if g:
         achieved = g["avg_bytes"] / (g["avg_ms"] * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "r1_c4_pmc_traffic.json")
+        if args.config == "c4" and os.path.exists(pmc):
+            # HBM bytes per launch of this kernel at this workload, from the
+            # committed rocprofv3 PMC passes (2*FETCH_SIZE + WRITE_SIZE).
+            with open(pmc) as fh:
+                traffic = int(json.load(fh)["gather_fwd_c4"]["hbm_bytes_per_launch"])
         roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
+                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
+                    traffic_unit="bytes/launch (PMC, profiles/r1_c4_pmc_traffic.json)",
                     kernel="gather_rows_kernel (forward mean aggregation)",
                     avg_ms=round(g["avg_ms"], 4), launches=g["launches"],
                     bytes_per_launch=int(g["avg_bytes"]))

@@ -189,14 +189,33 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
   }
 }
 
+// out[j] = sum_p partials[p][j]: a block owns 32 columns; its 8 row groups sum
+// the partials p == g (mod 8) (4 loads in flight each), then one thread adds
+// the 8 group sums in order: fixed order, deterministic.
 __global__ __launch_bounds__(kBlock) void colsum_kernel(const float* __restrict__ partials,
                                                         int np, int64_t width,
                                                         float* __restrict__ out) {
-  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (j >= width) return;
-  float s = 0.0f;
-  for (int p = 0; p < np; ++p) s += partials[(int64_t)p * width + j];
-  out[j] = s;
+  __shared__ float acc[8][32];
+  const int c = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int64_t j = (int64_t)blockIdx.x * 32 + c;
+  const int64_t jj = j < width ? j : width - 1;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int p = g;
+  for (; p + 24 < np; p += 32) {
+    s0 += partials[(int64_t)p * width + jj];
+    s1 += partials[(int64_t)(p + 8) * width + jj];
+    s2 += partials[(int64_t)(p + 16) * width + jj];
+    s3 += partials[(int64_t)(p + 24) * width + jj];
+  }
+  for (; p < np; p += 8) s0 += partials[(int64_t)p * width + jj];
+  acc[g][c] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (g == 0 && j < width) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += acc[k][c];
+    out[j] = s;
+  }
 }
 
 struct RowGeom {
@@ -383,7 +402,7 @@ extern "C" int sldm_colsum(const float* partials, int num_partials, int64_t widt
   SLDM_REQUIRE(num_partials >= 1 && width >= 0 && partials && out, "sldm_colsum: bad arguments");
   if (width == 0) return SLDM_OK;
   hipStream_t stream = sldm::as_stream(stream_);
-  colsum_kernel<<<(unsigned)((width + kBlock - 1) / kBlock), kBlock, 0, stream>>>(
+  colsum_kernel<<<(unsigned)((width + 31) / 32), kBlock, 0, stream>>>(
       partials, num_partials, width, out);
   SLDM_LAUNCH_CHECK("colsum_kernel");
   return SLDM_OK;
