@@ -43,7 +43,10 @@ CONFIGS = {
            "C3 1M nodes / 10M edges, F=256, 3 layers, bf16"),
     "c4": (10_000_000, 100_000_000, 256, 2, torch.bfloat16,
            "C4 10M nodes / 100M edges, F=256, 2 layers, bf16"),
+    "c5": (5_000_000, 80_000_000, 256, 2, torch.bfloat16,
+           "C5 5M nodes / 80M edges power-law in-degree (max ~10k), F=256, 2 layers, bf16"),
 }
+ZIPF_A = 0.47   # dst rank ~ k^-a over N ranks: max in-degree ~ E*(2^(1-a)-1)/(N^(1-a)-1) ~ 10k at C5
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -66,10 +69,29 @@ class KernelTimer:
         return out
 
 
-def make_graph(n, e, f, dtype, device, seed=0):
+def make_graph(n, e, f, dtype, device, seed=0, kind="uniform", p_local=0.9, blocks=8):
+    """SURVEY.md §8d synthetic graph: src, dst uniform in [0, N) (duplicates and
+    self loops allowed).  kind="local" is the locality-structured variant: dst
+    uniform, src drawn from dst's own block (N split into `blocks` contiguous
+    ranges = the 8-GPU partition) with probability p_local, else uniform."""
     g = torch.Generator(device=device).manual_seed(seed)
     src = torch.randint(0, n, (e,), generator=g, device=device)
     dst = torch.randint(0, n, (e,), generator=g, device=device)
+    if kind == "powerlaw":
+        # SURVEY.md §8d C5: dst from a truncated power law over ranks, ids
+        # permuted by a seeded randperm so hubs are scattered; src uniform.
+        u = torch.rand(e, generator=g, device=device, dtype=torch.float64)
+        b = 1.0 - ZIPF_A
+        rank_ = ((1.0 + u * (n ** b - 1.0)) ** (1.0 / b)).floor().long() - 1
+        perm = torch.randperm(n, generator=g, device=device)
+        dst = perm[rank_.clamp_(0, n - 1)]
+    if kind == "local":
+        P = (n + blocks - 1) // blocks
+        b0 = torch.div(dst, P, rounding_mode="floor") * P
+        span = torch.clamp(n - b0, max=P)
+        loc = b0 + (torch.rand(e, generator=g, device=device) * span).long().clamp(max=n - 1)
+        keep = torch.rand(e, generator=g, device=device) < p_local
+        src = torch.where(keep, loc, src)
     x = torch.randn(n, f, generator=g, device=device).to(dtype)
     return torch.stack([src, dst]), x
 
@@ -113,14 +135,27 @@ def main():
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--graph", default=None, choices=["uniform", "local", "powerlaw"],
+                    help="uniform (headline), the locality-structured variant, or power-law "
+                         "in-degrees (default for c5)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the partitioned (multi-GPU) path even on one GPU")
     args = ap.parse_args()
 
+    if args.graph is None:
+        args.graph = "powerlaw" if args.config == "c5" else "uniform"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_dist = world > 1 or args.force_dist
+    if use_dist:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
 
@@ -128,18 +163,25 @@ def main():
 
     cfg = CONFIGS[args.config]
     n, e, f, L, dtype, desc = cfg
-    ei, x = make_graph(n, e, f, dtype, dev)
+    ei, x = make_graph(n, e, f, dtype, dev, kind=args.graph)
     torch.manual_seed(0)
     blk = SageBlock([f] * (L + 1), dropout=0.25, negative_slope=0.1).to(dev).train()
     gout = torch.randn(n, f, device=dev, generator=torch.Generator(device=dev).manual_seed(2)
                        ).to(dtype)
 
-    if world > 1:
+    dist_info = {}
+    if use_dist:
         from sldm_sage.dist import DistSageBlock, partition_graph
         part = partition_graph(ei, n, world, rank)
         model = DistSageBlock(blk, part)
         x_in = x[part.row_begin:part.row_end].contiguous()
         g_in = gout[part.row_begin:part.row_end].contiguous()
+        hf, hb = part.halo_rows()
+        cross = float((part.fwd.col.long() >= part.num_rows).float().mean()) if part.fwd.num_edges else 0.0
+        dist_info = {"halo_rows_fwd_rank0": hf, "halo_rows_bwd_rank0": hb,
+                     "cross_partition_edge_fraction_rank0": round(cross, 4)}
+        del ei, x, gout
+        torch.cuda.empty_cache()
 
         def step():
             xr = x_in.detach().requires_grad_(True)
@@ -179,7 +221,7 @@ def main():
 
     # CSR-build-inclusive step (N=1: static-graph cache cleared once)
     incl = None
-    if world == 1:
+    if world == 1 and not use_dist:
         graph_cache.clear()
         barrier()
         t1 = time.perf_counter()
@@ -226,17 +268,21 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
-            "data": "synthetic (uniform random src/dst, x~N(0,1), random-init weights)",
-            "config": {"workload": desc, "nodes": n, "edges": e, "feat": f, "layers": L,
-                       "dropout": 0.25, "negative_slope": 0.1,
-                       "parallelism": f"dst-partition x{world}" if world > 1 else "single"},
+            "data": {"uniform": "synthetic (uniform random src/dst",
+                     "local": "synthetic (locality variant: src in dst's 1/8 block w.p. 0.9",
+                     "powerlaw": f"synthetic (dst Zipf a={ZIPF_A} over permuted ids, src uniform"
+                     }[args.graph] + ", x~N(0,1), random-init weights)",
+            "config": {"workload": desc, "graph": args.graph, "nodes": n, "edges": e, "feat": f,
+                       "layers": L, "dropout": 0.25, "negative_slope": 0.1,
+                       "parallelism": (f"dst-partition x{world}, RCCL halo all-to-all"
+                                       if use_dist else "single"), **dist_info},
             "value_incl_csr_build": round(incl, 1) if incl else None,
             "roofline": roof,
             "kernels": kernels,
             "cpu_baseline": base,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         torch.distributed.destroy_process_group()
 
 

@@ -57,6 +57,14 @@ int sldm_csr_build(const void* edge_index, int index_is_int64, int64_t num_edges
                    int32_t* t_rowptr, int32_t* t_col, int32_t* bad_index_flag,
                    void* workspace, size_t workspace_bytes, void* stream);
 
+/* Longest-first row schedule for skewed (power-law) graphs: order[s] = the
+ * row with the s-th largest rowptr degree (stable).  Gathering rows in this
+ * order starts hub rows first and pairs rows of similar length in a wave;
+ * results are unchanged (each row is still summed in CSR order). */
+size_t sldm_degree_order_workspace_bytes(int64_t num_nodes);
+int sldm_degree_order(const int32_t* rowptr, int64_t num_nodes, int32_t* order,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
 /* ----------------------------------------------------------- aggregation ---
  * out[i,:] = (addend[i,:] if addend) + S_i   with
  *   S_i = sum_{k in [rowptr[i], rowptr[i+1])} x[col[k], :]       (mean == 0)
@@ -67,9 +75,10 @@ int sldm_csr_build(const void* edge_index, int index_is_int64, int64_t num_edges
  * MeanAggregation / utils.scatter(reduce='mean').
  * Backward (mean=0, transpose CSR, x = inv_deg-prescaled dAgg, addend = the
  * lin_r input gradient) replaces autograd's gather + index_add_ (A8).
- * addend may be NULL; it has out's dtype. */
+ * addend may be NULL; it has out's dtype.  row_order (nullable) is a row
+ * schedule: slot s processes row row_order[s] (see sldm_degree_order). */
 int sldm_gather_rows(int x_dtype, const void* x, int64_t ldx,
-                     const int32_t* rowptr, const int32_t* col,
+                     const int32_t* rowptr, const int32_t* col, const int32_t* row_order,
                      int64_t num_rows, int64_t feat, int mean,
                      const void* addend, int64_t ld_add,
                      int out_dtype, void* out, int64_t ldo, void* stream);

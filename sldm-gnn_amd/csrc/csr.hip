@@ -47,6 +47,15 @@ __global__ __launch_bounds__(kBlock) void rowptr_from_sorted_kernel(
   for (int64_t k = prev + 1; k <= cur; ++k) rowptr[k] = (int32_t)p;
 }
 
+__global__ __launch_bounds__(kBlock) void degree_iota_kernel(const int32_t* __restrict__ rowptr,
+                                                             int64_t N, uint32_t* __restrict__ deg,
+                                                             uint32_t* __restrict__ ids) {
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= N) return;
+  deg[i] = (uint32_t)(rowptr[i + 1] - rowptr[i]);
+  ids[i] = (uint32_t)i;
+}
+
 unsigned key_bits(int64_t N) {
   unsigned bits = 0;
   while (bits < 32 && ((int64_t)1 << bits) < N) ++bits;
@@ -65,6 +74,52 @@ size_t sort_temp_bytes(int64_t E, int64_t N) {
 }
 
 }  // namespace
+
+// ------------------------------------------------------------------------
+// Longest-first row schedule for skewed (power-law) graphs: order = rows by
+// decreasing degree (stable).  The gather kernels walk rows in this order, so
+// hub rows start first and the rows sharing a wave have similar lengths;
+// every row is still summed sequentially in CSR order.
+namespace {
+size_t order_temp_bytes(int64_t N) {
+  size_t bytes = 0;
+  (void)rocprim::radix_sort_pairs_desc(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                       (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)N,
+                                       0u, 32u, (hipStream_t)0);
+  return bytes;
+}
+}  // namespace
+
+extern "C" size_t sldm_degree_order_workspace_bytes(int64_t num_nodes) {
+  if (num_nodes <= 0) return 256;
+  return 3 * align_up(sizeof(uint32_t) * (size_t)num_nodes) + align_up(order_temp_bytes(num_nodes)) + 256;
+}
+
+extern "C" int sldm_degree_order(const int32_t* rowptr, int64_t num_nodes, int32_t* order,
+                                 void* workspace, size_t workspace_bytes, void* stream_) {
+  const int64_t N = num_nodes;
+  SLDM_REQUIRE(N >= 0 && N < ((int64_t)1 << 31), "sldm_degree_order: bad N=%lld", (long long)N);
+  if (N == 0) return SLDM_OK;
+  SLDM_REQUIRE(rowptr && order, "sldm_degree_order: NULL argument");
+  const size_t need = sldm_degree_order_workspace_bytes(N);
+  SLDM_REQUIRE(workspace && workspace_bytes >= need,
+               "sldm_degree_order: workspace too small (%zu < %zu)", workspace_bytes, need);
+  hipStream_t stream = sldm::as_stream(stream_);
+  char* ws = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(workspace) + 255) & ~(uintptr_t)255);
+  const size_t arr = align_up(sizeof(uint32_t) * (size_t)N);
+  uint32_t* deg = reinterpret_cast<uint32_t*>(ws);
+  uint32_t* ids = reinterpret_cast<uint32_t*>(ws + arr);
+  uint32_t* deg_out = reinterpret_cast<uint32_t*>(ws + 2 * arr);
+  void* temp = ws + 3 * arr;
+  size_t temp_bytes = order_temp_bytes(N);
+  degree_iota_kernel<<<(unsigned)((N + kBlock - 1) / kBlock), kBlock, 0, stream>>>(rowptr, N, deg, ids);
+  SLDM_LAUNCH_CHECK("degree_iota_kernel");
+  SLDM_HIP_CHECK(rocprim::radix_sort_pairs_desc(temp, temp_bytes, (const uint32_t*)deg, deg_out,
+                                                (const uint32_t*)ids,
+                                                reinterpret_cast<uint32_t*>(order), (size_t)N,
+                                                0u, 32u, stream));
+  return SLDM_OK;
+}
 
 extern "C" size_t sldm_csr_workspace_bytes(int64_t num_edges, int64_t num_nodes) {
   if (num_edges < 0 || num_nodes < 0) return 0;

@@ -29,12 +29,15 @@ constexpr int kBlock = 256;
 template <typename TI, typename TO, int V, int NCH, bool MEAN, bool ADD>
 __global__ __launch_bounds__(kBlock) void gather_rows_kernel(
     const TI* __restrict__ x, int64_t ldx, const int32_t* __restrict__ rowptr,
-    const int32_t* __restrict__ col, int64_t nrows, int feat, int lpr_log2,
+    const int32_t* __restrict__ col, const int32_t* __restrict__ order, int64_t nrows,
+    int feat, int lpr_log2,
     const TO* __restrict__ addend, int64_t lda, TO* __restrict__ out, int64_t ldo) {
   const int lpr = 1 << lpr_log2;
   const int lane_in_row = threadIdx.x & (lpr - 1);
-  const int64_t row = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> lpr_log2;
-  if (row >= nrows) return;
+  const int64_t ridx = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> lpr_log2;
+  if (ridx >= nrows) return;
+  // Optional longest-first schedule (skewed graphs): slot ridx handles row order[ridx].
+  const int64_t row = order ? (int64_t)order[ridx] : ridx;
 
   int f0[NCH];
   bool act[NCH];
@@ -100,7 +103,7 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(
 }
 
 template <typename TI, typename TO, int V, bool MEAN, bool ADD>
-int launch_nch(const TI* x, int64_t ldx, const int32_t* rowptr, const int32_t* col,
+int launch_nch(const TI* x, int64_t ldx, const int32_t* rowptr, const int32_t* col, const int32_t* order,
                int64_t nrows, int feat, const TO* addend, int64_t lda, TO* out, int64_t ldo,
                hipStream_t stream) {
   int lpr = sldm::lanes_per_row(feat, V);
@@ -113,7 +116,7 @@ int launch_nch(const TI* x, int64_t ldx, const int32_t* rowptr, const int32_t* c
 #define SLDM_GATHER_CASE(NC)                                                            \
   case NC:                                                                              \
     gather_rows_kernel<TI, TO, V, NC, MEAN, ADD><<<(unsigned)grid, kBlock, 0, stream>>>( \
-        x, ldx, rowptr, col, nrows, feat, lpr_log2, addend, lda, out, ldo);             \
+        x, ldx, rowptr, col, order, nrows, feat, lpr_log2, addend, lda, out, ldo);             \
     break;
   switch (nch) {
     SLDM_GATHER_CASE(1)
@@ -130,7 +133,7 @@ int launch_nch(const TI* x, int64_t ldx, const int32_t* rowptr, const int32_t* c
 }
 
 template <typename TI, typename TO, bool MEAN, bool ADD>
-int launch_vec(int v, const void* x, int64_t ldx, const int32_t* rowptr, const int32_t* col,
+int launch_vec(int v, const void* x, int64_t ldx, const int32_t* rowptr, const int32_t* col, const int32_t* order,
                int64_t nrows, int feat, const void* addend, int64_t lda, void* out, int64_t ldo,
                hipStream_t stream) {
   auto xi = reinterpret_cast<const TI*>(x);
@@ -139,33 +142,34 @@ int launch_vec(int v, const void* x, int64_t ldx, const int32_t* rowptr, const i
   switch (v) {
     case 8:
       if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2)
-        return launch_nch<TI, TO, 8, MEAN, ADD>(xi, ldx, rowptr, col, nrows, feat, ad, lda, o, ldo, stream);
+        return launch_nch<TI, TO, 8, MEAN, ADD>(xi, ldx, rowptr, col, order, nrows, feat, ad, lda, o, ldo, stream);
       break;
     case 4:
-      return launch_nch<TI, TO, 4, MEAN, ADD>(xi, ldx, rowptr, col, nrows, feat, ad, lda, o, ldo, stream);
+      return launch_nch<TI, TO, 4, MEAN, ADD>(xi, ldx, rowptr, col, order, nrows, feat, ad, lda, o, ldo, stream);
     case 2:
-      return launch_nch<TI, TO, 2, MEAN, ADD>(xi, ldx, rowptr, col, nrows, feat, ad, lda, o, ldo, stream);
+      return launch_nch<TI, TO, 2, MEAN, ADD>(xi, ldx, rowptr, col, order, nrows, feat, ad, lda, o, ldo, stream);
     case 1:
-      return launch_nch<TI, TO, 1, MEAN, ADD>(xi, ldx, rowptr, col, nrows, feat, ad, lda, o, ldo, stream);
+      return launch_nch<TI, TO, 1, MEAN, ADD>(xi, ldx, rowptr, col, order, nrows, feat, ad, lda, o, ldo, stream);
   }
   sldm::set_error("sldm_gather_rows: unsupported vector width %d", v);
   return SLDM_ERR_ARG;
 }
 
 template <typename T, bool MEAN, bool ADD>
-int dispatch_same(const void* x, int64_t ldx, const int32_t* rowptr, const int32_t* col,
+int dispatch_same(const void* x, int64_t ldx, const int32_t* rowptr, const int32_t* col, const int32_t* order,
                   int64_t nrows, int feat, const void* addend, int64_t lda, void* out,
                   int64_t ldo, hipStream_t stream) {
   int v = sldm::pick_vec((int)sizeof(T), feat, {ldx, ldo, ADD ? lda : (int64_t)0},
                          {x, out, addend});
-  return launch_vec<T, T, MEAN, ADD>(v, x, ldx, rowptr, col, nrows, feat, addend, lda, out, ldo,
+  return launch_vec<T, T, MEAN, ADD>(v, x, ldx, rowptr, col, order, nrows, feat, addend, lda, out, ldo,
                                      stream);
 }
 
 }  // namespace
 
 extern "C" int sldm_gather_rows(int x_dtype, const void* x, int64_t ldx, const int32_t* rowptr,
-                                const int32_t* col, int64_t num_rows, int64_t feat, int mean,
+                                const int32_t* col, const int32_t* row_order,
+                                int64_t num_rows, int64_t feat, int mean,
                                 const void* addend, int64_t ld_add, int out_dtype, void* out,
                                 int64_t ldo, void* stream_) {
   SLDM_REQUIRE(x_dtype == out_dtype && (x_dtype == SLDM_F32 || x_dtype == SLDM_BF16),
@@ -183,16 +187,16 @@ extern "C" int sldm_gather_rows(int x_dtype, const void* x, int64_t ldx, const i
   const bool add = addend != nullptr;
   if (x_dtype == SLDM_F32) {
     if (mean)
-      return add ? dispatch_same<float, true, true>(x, ldx, rowptr, col, num_rows, f, addend, ld_add, out, ldo, stream)
-                 : dispatch_same<float, true, false>(x, ldx, rowptr, col, num_rows, f, addend, ld_add, out, ldo, stream);
-    return add ? dispatch_same<float, false, true>(x, ldx, rowptr, col, num_rows, f, addend, ld_add, out, ldo, stream)
-               : dispatch_same<float, false, false>(x, ldx, rowptr, col, num_rows, f, addend, ld_add, out, ldo, stream);
+      return add ? dispatch_same<float, true, true>(x, ldx, rowptr, col, row_order, num_rows, f, addend, ld_add, out, ldo, stream)
+                 : dispatch_same<float, true, false>(x, ldx, rowptr, col, row_order, num_rows, f, addend, ld_add, out, ldo, stream);
+    return add ? dispatch_same<float, false, true>(x, ldx, rowptr, col, row_order, num_rows, f, addend, ld_add, out, ldo, stream)
+               : dispatch_same<float, false, false>(x, ldx, rowptr, col, row_order, num_rows, f, addend, ld_add, out, ldo, stream);
   }
   if (mean)
-    return add ? dispatch_same<uint16_t, true, true>(x, ldx, rowptr, col, num_rows, f, addend, ld_add, out, ldo, stream)
-               : dispatch_same<uint16_t, true, false>(x, ldx, rowptr, col, num_rows, f, addend, ld_add, out, ldo, stream);
-  return add ? dispatch_same<uint16_t, false, true>(x, ldx, rowptr, col, num_rows, f, addend, ld_add, out, ldo, stream)
-             : dispatch_same<uint16_t, false, false>(x, ldx, rowptr, col, num_rows, f, addend, ld_add, out, ldo, stream);
+    return add ? dispatch_same<uint16_t, true, true>(x, ldx, rowptr, col, row_order, num_rows, f, addend, ld_add, out, ldo, stream)
+               : dispatch_same<uint16_t, true, false>(x, ldx, rowptr, col, row_order, num_rows, f, addend, ld_add, out, ldo, stream);
+  return add ? dispatch_same<uint16_t, false, true>(x, ldx, rowptr, col, row_order, num_rows, f, addend, ld_add, out, ldo, stream)
+             : dispatch_same<uint16_t, false, false>(x, ldx, rowptr, col, row_order, num_rows, f, addend, ld_add, out, ldo, stream);
 }
 
 // ------------------------------------------------------------------------

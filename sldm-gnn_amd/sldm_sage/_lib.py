@@ -29,7 +29,9 @@ _SIGNATURES = {
     "sldm_csr_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
     "sldm_csr_build": (ctypes.c_int, [_vp, ctypes.c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp,
                                       _vp, _vp, ctypes.c_size_t, _vp]),
-    "sldm_gather_rows": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _vp, _vp, _c_i64, _c_i64,
+    "sldm_degree_order_workspace_bytes": (ctypes.c_size_t, [_c_i64]),
+    "sldm_degree_order": (ctypes.c_int, [_vp, _c_i64, _vp, _vp, ctypes.c_size_t, _vp]),
+    "sldm_gather_rows": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _vp, _vp, _vp, _c_i64, _c_i64,
                                         ctypes.c_int, _vp, _c_i64, ctypes.c_int, _vp, _c_i64,
                                         _vp]),
     "sldm_scale_rows_by_inv_deg": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _vp, _c_i64,

@@ -6,22 +6,25 @@ destination node because the mean aggregation of row i reads only i's
 in-edges, and the dense part, LayerNorm and activation are row-local.
 
 Rank r owns the contiguous node rows [r*P, min((r+1)*P, N)), P = ceil(N/W):
-  * its in-edges as a CSR by destination (rows = own nodes, col = GLOBAL
-    source ids) for the forward aggregation;
-  * its out-edges as a CSR by source (rows = own nodes, col = GLOBAL
-    destination ids) for the backward (transpose) aggregation.
+  * its in-edges as a CSR by destination (rows = own nodes) for the forward;
+  * its out-edges as a CSR by source (rows = own nodes) for the backward.
+Column ids are remapped at partition time into a per-rank *halo buffer*:
+positions [0, n_own) are the rank's own rows, the rest are the remote rows it
+actually references, grouped by owner (sorted).  A halo *plan* per direction
+holds, for every peer, which of our rows it needs (send list) and how many of
+its rows we receive; the lists are exchanged once, at partition time.
 Per layer:
-  forward   x_full = all_gather(x_local)          (RCCL, [W*P, F])
-            agg    = gather-mean over own in-edges from x_full
-            out    = dense + LayerNorm + act + dropout on own rows
+  forward   buf = [x_own | all_to_all_v(x_own[send_idx])]      (RCCL)
+            agg = gather-mean over own in-edges from buf
+            out = dense + LayerNorm + act + dropout on own rows
   backward  dh, [dAgg/deg | dx_root] on own rows
-            g_full = all_gather(dAgg/deg)          (RCCL, [W*P, F_in])
-            dx     = dx_root + transpose gather over own out-edges from g_full
+            buf = [g_own | all_to_all_v(g_own[send_idx])]       (second plan)
+            dx  = dx_root + transpose gather over own out-edges from buf
             weight grads: one bucketed all_reduce(SUM) per layer
-The all-gathered buffer is laid out rank-major with P rows per rank, so a
-global node id indexes it directly.  Rows are summed in the same CSR order
-as on one GPU, and dropout keys use global row ids, so W ranks reproduce the
-single-GPU result.
+Only referenced rows cross xGMI (on a uniform random graph with E/N = 10 and
+8 ranks that is ~71% of the remote rows; on a partition-local graph far
+fewer).  Each row's edges are summed in the same order as on one GPU and
+dropout keys use global row ids, so W ranks reproduce the single-GPU result.
 
 The per-rank compute goes through a backend object (default: the HIP ops);
 the CPU tests plug a plain-torch backend in to run the same protocol over
@@ -56,6 +59,12 @@ class HipBackend:
                                name="gather_fwd" if mean else "gather_bwd")
 
     @staticmethod
+    def pick_rows(x, rowptr, idx):
+        """x[idx] through the gather kernel (one-edge rows, no mean)."""
+        from . import ops
+        return ops.gather_rows(x, rowptr, idx, idx.numel(), mean=False, name="halo_pack")
+
+    @staticmethod
     def layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p, seed, save, row_offset):
         from . import dense
         return dense.sage_layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p, seed,
@@ -79,6 +88,20 @@ class HipBackend:
 
 
 @dataclass
+class HaloPlan:
+    """Which own rows go to which peer, and how many rows come back."""
+
+    send_idx: torch.Tensor        # local row ids, grouped by destination peer
+    send_rowptr: torch.Tensor     # identity CSR (arange) for the pack gather
+    send_counts: list[int]
+    recv_counts: list[int]
+
+    @property
+    def num_recv(self) -> int:
+        return sum(self.recv_counts)
+
+
+@dataclass
 class GraphPartition:
     """One rank's share of a graph (see module docstring)."""
 
@@ -88,50 +111,105 @@ class GraphPartition:
     rows_per_rank: int           # P
     row_begin: int
     row_end: int
-    fwd: SageGraph               # rows = own nodes (local), col = global sources
-    bwd: SageGraph               # rows = own nodes (local), col = global destinations
-    num_local_edges: int         # in-edges of own rows
+    fwd: SageGraph               # rows = own nodes, col = halo-buffer positions (sources)
+    bwd: SageGraph               # rows = own nodes, col = halo-buffer positions (destinations)
+    fwd_plan: HaloPlan
+    bwd_plan: HaloPlan
 
     @property
     def num_rows(self) -> int:
         return self.row_end - self.row_begin
 
+    def halo_rows(self) -> tuple[int, int]:
+        """(rows received in the forward exchange, in the backward exchange)."""
+        return self.fwd_plan.num_recv, self.bwd_plan.num_recv
+
+
+def _exchange_counts(counts: list[int], device, group) -> list[int]:
+    world = len(counts)
+    if world == 1:
+        return list(counts)
+    send = torch.tensor(counts, dtype=torch.int64, device=device)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    return recv.tolist()
+
+
+def _build_plan(ids: torch.Tensor, r0: int, r1: int, P: int, world: int, group):
+    """ids: global node ids this rank references (any order, duplicates ok).
+
+    Returns (remap, plan): remap(global ids) -> halo-buffer positions."""
+    dev = ids.device
+    uniq = torch.unique(ids)                                   # sorted
+    remote = uniq[(uniq < r0) | (uniq >= r1)]                  # sorted => grouped by owner
+    owner = torch.div(remote, P, rounding_mode="floor")
+    need_counts = torch.bincount(owner, minlength=world)[:world].tolist()
+    give_counts = _exchange_counts(need_counts, dev, group)
+    # tell each owner which of its rows we need (global ids), learn what to send
+    if world > 1:
+        wanted = torch.empty(sum(give_counts), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(wanted, remote.to(torch.int64).contiguous(),
+                               output_split_sizes=give_counts,
+                               input_split_sizes=need_counts, group=group)
+    else:
+        wanted = remote.to(torch.int64)
+    send_idx = (wanted - r0).to(torch.int32)
+    n_own = r1 - r0
+
+    def remap(g: torch.Tensor) -> torch.Tensor:
+        own = (g >= r0) & (g < r1)
+        pos = torch.searchsorted(remote, g)
+        return torch.where(own, g - r0, n_own + pos).to(torch.int32)
+
+    rowptr = torch.arange(send_idx.numel() + 1, dtype=torch.int32, device=dev)
+    return remap, HaloPlan(send_idx, rowptr, give_counts, need_counts)
+
 
 def partition_graph(edge_index: torch.Tensor, num_nodes: int, world: int, rank: int,
-                    backend=HipBackend) -> GraphPartition:
+                    backend=HipBackend, group=None) -> GraphPartition:
     """Build rank ``rank``'s partition from the full edge_index (same on every
-    rank; it may live on any device the backend accepts)."""
+    rank).  Collective over ``group`` (the halo lists are exchanged here)."""
     P = (num_nodes + world - 1) // world
     r0, r1 = min(rank * P, num_nodes), min((rank + 1) * P, num_nodes)
+    n = r1 - r0
     src, dst = edge_index[0], edge_index[1]
     ein = edge_index[:, (dst >= r0) & (dst < r1)]     # original order kept
     eout = edge_index[:, (src >= r0) & (src < r1)]
-    rp, col, _, _ = backend.csr(ein, num_nodes, False)
-    _, _, trp, tcol = backend.csr(eout, num_nodes, True)
-    n = r1 - r0
-    fwd = SageGraph(n, int(ein.size(1)), rp[r0:r1 + 1], col, None, None)
-    bwd = SageGraph(n, int(eout.size(1)), trp[r0:r1 + 1], tcol, None, None)
-    return GraphPartition(rank, world, num_nodes, P, r0, r1, fwd, bwd, int(ein.size(1)))
+    remap_f, plan_f = _build_plan(ein[0], r0, r1, P, world, group)
+    remap_b, plan_b = _build_plan(eout[1], r0, r1, P, world, group)
+    n_buf_f = n + plan_f.num_recv
+    n_buf_b = n + plan_b.num_recv
+    # CSR by (local) destination over buffer-position sources, and by (local)
+    # source over buffer-position destinations; stable, so edge order is kept.
+    fin = torch.stack([remap_f(ein[0]).long(), (ein[1] - r0).long()])
+    fout = torch.stack([(eout[0] - r0).long(), remap_b(eout[1]).long()])
+    rp, col, _, _ = backend.csr(fin, max(n_buf_f, 1), False)
+    _, _, trp, tcol = backend.csr(fout, max(n_buf_b, 1), True)
+    fwd = SageGraph(n, int(ein.size(1)), rp[: n + 1], col, None, None)
+    bwd = SageGraph(n, int(eout.size(1)), trp[: n + 1], tcol, None, None)
+    return GraphPartition(rank, world, num_nodes, P, r0, r1, fwd, bwd, plan_f, plan_b)
 
 
-def _all_gather_rows(x_local: torch.Tensor, part: GraphPartition, group) -> torch.Tensor:
-    """[n_local, F] -> [W*P, F], rank-major, P rows per rank (tail padded)."""
-    P, F = part.rows_per_rank, x_local.size(1)
-    if x_local.size(0) != P:
-        padded = x_local.new_zeros(P, F)
-        padded[: x_local.size(0)] = x_local
-        x_local = padded
-    out = x_local.new_empty(part.world * P, F)
-    dist.all_gather_into_tensor(out, x_local.contiguous(), group=group)
-    return out
+def _halo_buffer(x_own: torch.Tensor, plan: HaloPlan, backend, group) -> torch.Tensor:
+    """[x_own ; rows received from peers] (the layout the remapped CSR indexes)."""
+    n, F = x_own.shape
+    buf = x_own.new_empty(n + plan.num_recv, F)
+    buf[:n].copy_(x_own)
+    if plan.num_recv or sum(plan.send_counts):
+        send = (backend.pick_rows(x_own, plan.send_rowptr, plan.send_idx)
+                if plan.send_idx.numel() else x_own.new_empty(0, F))
+        dist.all_to_all_single(buf[n:], send, output_split_sizes=plan.recv_counts,
+                               input_split_sizes=plan.send_counts, group=group)
+    return buf
 
 
 class _DistLayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wl, bl, wr, gamma, beta, part: GraphPartition, group, backend,
                 slope, drop_p, seed, eps):
-        x_full = _all_gather_rows(x, part, group)
-        agg = backend.gather(x_full, part.fwd.rowptr, part.fwd.col, part.num_rows, True)
+        buf = _halo_buffer(x, part.fwd_plan, backend, group)
+        agg = backend.gather(buf, part.fwd.rowptr, part.fwd.col, part.num_rows, True)
+        del buf
         save = any(ctx.needs_input_grad[:6])
         out, xhat, rstd = backend.layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p,
                                             seed, save, part.row_begin)
@@ -150,14 +228,15 @@ class _DistLayerFn(torch.autograd.Function):
                                              drop_p, seed, out, part.row_begin)
         dwl, dwr = be.bwd_weight(dh, agg, x)
         # one bucketed all-reduce of this layer's weight gradients (fp32)
-        flat = torch.cat([t.reshape(-1).float() for t in (dwl, dbl, dwr, dgamma, dbeta)])
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
-        sizes = [t.numel() for t in (dwl, dbl, dwr, dgamma, dbeta)]
+        grads = (dwl, dbl, dwr, dgamma, dbeta)
+        flat = torch.cat([t.reshape(-1).float() for t in grads])
+        if part.world > 1:
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
         dwl, dbl, dwr, dgamma, dbeta = (c.view_as(t) for c, t in zip(
-            torch.split(flat, sizes), (dwl, dbl, dwr, dgamma, dbeta)))
+            torch.split(flat, [t.numel() for t in grads]), grads))
         g, dx_r = be.bwd_data(dh, wl, wr, part.fwd.rowptr)
-        g_full = _all_gather_rows(g.contiguous(), part, group)
-        dx = be.gather(g_full, part.bwd.rowptr, part.bwd.col, part.num_rows, False,
+        buf = _halo_buffer(g.contiguous(), part.bwd_plan, be, group)
+        dx = be.gather(buf, part.bwd.rowptr, part.bwd.col, part.num_rows, False,
                        addend=dx_r.contiguous())
         return (dx, dwl.to(wl.dtype), dbl.to(wl.dtype), dwr.to(wr.dtype), dgamma.to(gamma.dtype),
                 dbeta.to(beta.dtype), None, None, None, None, None, None, None)
@@ -170,7 +249,7 @@ class DistSageBlock(nn.Module):
     node features and returns the same rows of the block's output; after
     ``backward`` every rank holds the full (summed) parameter gradients,
     identical to a single-device run.  Parameters are broadcast from rank 0
-    at construction.
+    at construction.  Seed every rank identically (dropout draws).
     """
 
     def __init__(self, block: nn.Module, partition: GraphPartition, group=None,

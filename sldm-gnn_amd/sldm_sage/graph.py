@@ -30,6 +30,8 @@ class SageGraph:
     col: torch.Tensor               # [E]   sources, original edge order per row
     t_rowptr: torch.Tensor | None   # [N+1] by source (backward)
     t_col: torch.Tensor | None      # [E]   destinations
+    order: torch.Tensor | None = None     # longest-first schedule of rowptr rows (skewed graphs)
+    t_order: torch.Tensor | None = None   # same for t_rowptr
 
     @property
     def device(self) -> torch.device:
@@ -52,7 +54,23 @@ def build_graph(edge_index: torch.Tensor, num_nodes: int, transpose: bool = True
         raise IndexError(
             f"edge_index holds a node id outside [0, {num_nodes}) "
             "(the reference's index_select/scatter would raise as well)")
-    return SageGraph(num_nodes, int(edge_index.size(1)), rowptr, col, t_rowptr, t_col)
+    g = SageGraph(num_nodes, int(edge_index.size(1)), rowptr, col, t_rowptr, t_col)
+    g.order = _schedule(rowptr, g.num_edges)
+    if t_rowptr is not None:
+        g.t_order = _schedule(t_rowptr, g.num_edges)
+    return g
+
+
+def _schedule(rowptr: torch.Tensor, num_edges: int):
+    """Longest-first row order when the degree distribution is skewed
+    (max > max(64, 8 x mean)), e.g. power-law in-degrees; None otherwise."""
+    n = rowptr.numel() - 1
+    if n <= 0 or num_edges == 0:
+        return None
+    max_deg = int((rowptr[1:] - rowptr[:-1]).max().item())
+    if max_deg <= max(64, 8 * num_edges / n):
+        return None
+    return ops.degree_order(rowptr)
 
 
 class _GraphCache:

@@ -109,12 +109,28 @@ def csr_build(edge_index: torch.Tensor, num_nodes: int, transpose: bool = True):
     return rowptr, col, t_rowptr, t_col, bad
 
 
+def degree_order(rowptr: torch.Tensor) -> torch.Tensor:
+    """Rows by decreasing degree (stable): the longest-first gather schedule."""
+    dev = _require_gpu(rowptr)
+    n = rowptr.numel() - 1
+    lib = _lib.load()
+    order = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
+    ws_bytes = lib.sldm_degree_order_workspace_bytes(n)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    _lib.check(lib.sldm_degree_order(rowptr.data_ptr(), n, order.data_ptr(), ws.data_ptr(),
+                                     ws_bytes, _stream(dev)), "sldm_degree_order")
+    return order
+
+
 # ------------------------------------------------------------ aggregation --
 def gather_rows(x: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor, num_rows: int,
                 mean: bool, addend: torch.Tensor | None = None,
-                out: torch.Tensor | None = None, name: str = "gather") -> torch.Tensor:
-    """out[i] = (addend[i] +) sum_{k in row i} x[col[k]]  (/ max(1, deg_i) if mean)."""
-    dev = _require_gpu(x, rowptr, col, addend, out)
+                out: torch.Tensor | None = None, name: str = "gather",
+                order: torch.Tensor | None = None) -> torch.Tensor:
+    """out[i] = (addend[i] +) sum_{k in row i} x[col[k]]  (/ max(1, deg_i) if mean).
+
+    ``order`` (optional) is a row schedule from :func:`degree_order`."""
+    dev = _require_gpu(x, rowptr, col, addend, out, order)
     if x.dim() != 2 or x.stride(1) != 1:
         x = x.contiguous()
     F = x.size(1)
@@ -131,7 +147,7 @@ def gather_rows(x: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor, num_ro
     with _Timed(name, bytes_alg):
         _lib.check(_lib.load().sldm_gather_rows(
             dtype_code(x), x.data_ptr(), x.stride(0), rowptr.data_ptr(),
-            col.data_ptr() if E else rowptr.data_ptr(), num_rows, F, int(bool(mean)),
+            col.data_ptr() if E else rowptr.data_ptr(), _ptr(order), num_rows, F, int(bool(mean)),
             _ptr(addend), addend.stride(0) if addend is not None else 0,
             dtype_code(out), out.data_ptr(), out.stride(0), _stream(dev)), "sldm_gather_rows")
     return out

@@ -59,7 +59,8 @@ class _SageLayerFn(torch.autograd.Function):
     def forward(ctx, x, wl, bl, wr, gamma, beta, graph: SageGraph, slope: float, drop_p: float,
                 seed: int, eps: float):
         n = x.size(0)
-        agg = ops.gather_rows(x, graph.rowptr, graph.col, n, mean=True, name="gather_fwd")
+        agg = ops.gather_rows(x, graph.rowptr, graph.col, n, mean=True, name="gather_fwd",
+                              order=graph.order)
         needs_grad = any(ctx.needs_input_grad[:6])
         out, xhat, rstd = dense.sage_layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope,
                                                drop_p, seed, save=needs_grad)
@@ -88,6 +89,7 @@ class _SageLayerFn(torch.autograd.Function):
             # adds the root-path gradient as it sums over out-edges.
             g, dx_r = dense.sage_linear_bwd_data(dh, wl, wr, graph.rowptr)
             dx = ops.gather_rows(g, graph.t_rowptr, graph.t_col, x.size(0), mean=False,
+                                 order=graph.t_order,
                                  addend=dx_r, name="gather_bwd")
         return (dx, dwl.to(wl.dtype), dbl.to(wl.dtype), dwr.to(wr.dtype),
                 dgamma.to(gamma.dtype), dbeta.to(beta.dtype), None, None, None, None, None)
@@ -129,7 +131,7 @@ class _MeanAggFn(torch.autograd.Function):
     def forward(ctx, x, graph: SageGraph):
         ctx.graph = graph
         ctx.n = x.size(0)
-        return ops.gather_rows(x, graph.rowptr, graph.col, x.size(0), mean=True,
+        return ops.gather_rows(x, graph.rowptr, graph.col, x.size(0), mean=True, order=graph.order,
                                name="gather_fwd")
 
     @staticmethod
@@ -137,7 +139,7 @@ class _MeanAggFn(torch.autograd.Function):
         graph = ctx.graph
         g = g.contiguous().clone()
         ops.scale_rows_by_inv_deg_(g, graph.rowptr)
-        return ops.gather_rows(g, graph.t_rowptr, graph.t_col, ctx.n, mean=False,
+        return ops.gather_rows(g, graph.t_rowptr, graph.t_col, ctx.n, mean=False, order=graph.t_order,
                                name="gather_bwd"), None
 
 

@@ -41,6 +41,10 @@ class CpuBackend:
         return out.to(x.dtype)
 
     @staticmethod
+    def pick_rows(x, rowptr, idx):
+        return x[idx.long()]
+
+    @staticmethod
     def layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p, seed, save, row_offset):
         assert drop_p == 0.0, "CPU test backend has no dropout"
         h = agg @ wl.detach().t() + bl.detach() + x @ wr.detach().t()

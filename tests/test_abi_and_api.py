@@ -39,7 +39,7 @@ def test_error_reporting_without_gpu():
     """Argument validation fails before any device work and sets the message."""
     from sldm_sage import _lib
     lib = _lib.load()
-    rc = lib.sldm_gather_rows(0, None, 16, None, None, 10, 16, 1, None, 0, 1, None, 16, None)
+    rc = lib.sldm_gather_rows(0, None, 16, None, None, None, 10, 16, 1, None, 0, 1, None, 16, None)
     assert rc != 0
     assert b"dtypes" in lib.sldm_last_error()
     with pytest.raises(_lib.SldmError):

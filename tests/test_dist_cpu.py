@@ -65,7 +65,7 @@ def _worker(rank, world, port, hdims, n, e, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 300), (3, 301)])
+@pytest.mark.parametrize("world,n", [(2, 300), (3, 301), (4, 97)])
 def test_dist_sageblock_matches_single_device(world, n):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -55,6 +55,59 @@ def test_csr_power_law_hub():
     assert np.array_equal(g.t_rowptr.cpu().numpy(), trp) and np.array_equal(g.t_col.cpu().numpy(), tcol)
 
 
+def _powerlaw_graph(n, e, a=0.47, seed=7):
+    g = torch.Generator().manual_seed(seed)
+    u = torch.rand(e, generator=g, dtype=torch.float64)
+    b = 1.0 - a
+    rank = ((1.0 + u * (n ** b - 1.0)) ** (1.0 / b)).floor().long().clamp(1, n) - 1
+    dst = torch.randperm(n, generator=g)[rank]
+    src = torch.randint(0, n, (e,), generator=g)
+    return torch.stack([src, dst])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gather_powerlaw_schedule_bit_exact(dtype):
+    """Skewed in-degrees switch on the longest-first schedule; sums unchanged."""
+    from sldm_sage import build_graph, ops
+    n, e, f = 20_000, 300_000, 128
+    ei = _powerlaw_graph(n, e)
+    x = torch.randn(n, f, generator=torch.Generator().manual_seed(1)).to(dtype)
+    g = build_graph(ei.to(DEV), n)
+    deg = torch.bincount(ei[1], minlength=n)
+    assert g.order is not None and int(deg.max()) > 1000
+    order = g.order.cpu().long()
+    assert torch.equal(deg[order], torch.sort(deg, descending=True, stable=True).values)
+    assert torch.equal(torch.sort(order).values, torch.arange(n))
+    out = ops.gather_rows(x.to(DEV), g.rowptr, g.col, n, mean=True, order=g.order)
+    rp, col, _, _ = ref_csr(ei, n)
+    ref = ref_agg_mean_f32(x.float(), rp, col).to(dtype)
+    assert torch.equal(out.cpu(), ref)
+    # without the schedule: identical result
+    out2 = ops.gather_rows(x.to(DEV), g.rowptr, g.col, n, mean=True)
+    assert torch.equal(out, out2)
+
+
+def test_sageblock_powerlaw_fwd_bwd():
+    from sldm_sage import SageBlock
+    n, e, hd = 5000, 60_000, [32, 32, 32]
+    ei = _powerlaw_graph(n, e, seed=3)
+    x = torch.randn(n, hd[0], generator=torch.Generator().manual_seed(2))
+    gout = torch.randn(n, hd[-1], generator=torch.Generator().manual_seed(3))
+    ref = oracle_block(hd, 0.1)
+    out_r, dx_r, gr = run_oracle(ref, x, ei, gout)
+    blk = SageBlock(hd, None, 0.1)
+    blk.load_state_dict(ref.state_dict())
+    blk = blk.to(DEV)
+    xg = x.to(DEV).requires_grad_(True)
+    out = blk(xg, ei.to(DEV))
+    out.backward(gout.to(DEV))
+    torch.testing.assert_close(out.detach().cpu(), out_r, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(xg.grad.cpu(), dx_r, atol=1e-4, rtol=1e-4)
+    for k, p in blk.named_parameters():
+        s = max(1.0, gr[k].abs().max().item())
+        torch.testing.assert_close(p.grad.cpu() / s, gr[k] / s, atol=1e-4, rtol=1e-4)
+
+
 @pytest.mark.parametrize("bad", [-1, 50])
 def test_csr_bad_index_raises(bad):
     from sldm_sage import build_graph
