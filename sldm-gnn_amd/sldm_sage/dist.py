@@ -190,17 +190,24 @@ def partition_graph(edge_index: torch.Tensor, num_nodes: int, world: int, rank: 
     return GraphPartition(rank, world, num_nodes, P, r0, r1, fwd, bwd, plan_f, plan_b)
 
 
-def _halo_buffer(x_own: torch.Tensor, plan: HaloPlan, backend, group) -> torch.Tensor:
-    """[x_own ; rows received from peers] (the layout the remapped CSR indexes)."""
+def _halo_buffer(x_own: torch.Tensor, plan: HaloPlan, backend, group, async_op=False):
+    """[x_own ; rows received from peers] (the layout the remapped CSR indexes).
+
+    With ``async_op`` returns (buf, work): the exchange runs on RCCL's stream
+    while the caller queues independent kernels; ``work.wait()`` before use."""
     n, F = x_own.shape
+    if plan.num_recv == 0 and sum(plan.send_counts) == 0:
+        return (x_own, None) if async_op else x_own   # nothing crosses: no copy
     buf = x_own.new_empty(n + plan.num_recv, F)
     buf[:n].copy_(x_own)
+    work = None
     if plan.num_recv or sum(plan.send_counts):
         send = (backend.pick_rows(x_own, plan.send_rowptr, plan.send_idx)
                 if plan.send_idx.numel() else x_own.new_empty(0, F))
-        dist.all_to_all_single(buf[n:], send, output_split_sizes=plan.recv_counts,
-                               input_split_sizes=plan.send_counts, group=group)
-    return buf
+        work = dist.all_to_all_single(buf[n:], send, output_split_sizes=plan.recv_counts,
+                                      input_split_sizes=plan.send_counts, group=group,
+                                      async_op=async_op)
+    return (buf, work) if async_op else buf
 
 
 class _DistLayerFn(torch.autograd.Function):
@@ -226,18 +233,25 @@ class _DistLayerFn(torch.autograd.Function):
         slope, drop_p, seed = ctx.cfg
         dh, dgamma, dbeta, dbl = be.post_bwd(dout.contiguous(), xhat, rstd, gamma, beta, slope,
                                              drop_p, seed, out, part.row_begin)
+        # dAgg/deg first, so its halo exchange (RCCL stream) overlaps the
+        # weight-gradient GEMM and all-reduce queued behind it.
+        g, dx_r = be.bwd_data(dh, wl, wr, part.fwd.rowptr)
+        buf, xwork = _halo_buffer(g.contiguous(), part.bwd_plan, be, group, async_op=True)
         dwl, dwr = be.bwd_weight(dh, agg, x)
         # one bucketed all-reduce of this layer's weight gradients (fp32)
         grads = (dwl, dbl, dwr, dgamma, dbeta)
         flat = torch.cat([t.reshape(-1).float() for t in grads])
+        rwork = None
         if part.world > 1:
-            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
-        dwl, dbl, dwr, dgamma, dbeta = (c.view_as(t) for c, t in zip(
-            torch.split(flat, [t.numel() for t in grads]), grads))
-        g, dx_r = be.bwd_data(dh, wl, wr, part.fwd.rowptr)
-        buf = _halo_buffer(g.contiguous(), part.bwd_plan, be, group)
+            rwork = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group, async_op=True)
+        if xwork is not None:
+            xwork.wait()
         dx = be.gather(buf, part.bwd.rowptr, part.bwd.col, part.num_rows, False,
                        addend=dx_r.contiguous())
+        if rwork is not None:
+            rwork.wait()
+        dwl, dbl, dwr, dgamma, dbeta = (c.view_as(t) for c, t in zip(
+            torch.split(flat, [t.numel() for t in grads]), grads))
         return (dx, dwl.to(wl.dtype), dbl.to(wl.dtype), dwr.to(wr.dtype), dgamma.to(gamma.dtype),
                 dbeta.to(beta.dtype), None, None, None, None, None, None, None)
 

@@ -11,6 +11,7 @@ entry, and nothing outlives the edge_index tensor it describes.
 """
 from __future__ import annotations
 
+import os
 import threading
 import weakref
 from dataclasses import dataclass
@@ -65,7 +66,7 @@ def _schedule(rowptr: torch.Tensor, num_edges: int):
     """Longest-first row order when the degree distribution is skewed
     (max > max(64, 8 x mean)), e.g. power-law in-degrees; None otherwise."""
     n = rowptr.numel() - 1
-    if n <= 0 or num_edges == 0:
+    if n <= 0 or num_edges == 0 or os.environ.get("SLDM_NO_SCHEDULE") == "1":
         return None
     max_deg = int((rowptr[1:] - rowptr[:-1]).max().item())
     if max_deg <= max(64, 8 * num_edges / n):

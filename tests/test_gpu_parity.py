@@ -74,7 +74,7 @@ def test_gather_powerlaw_schedule_bit_exact(dtype):
     x = torch.randn(n, f, generator=torch.Generator().manual_seed(1)).to(dtype)
     g = build_graph(ei.to(DEV), n)
     deg = torch.bincount(ei[1], minlength=n)
-    assert g.order is not None and int(deg.max()) > 1000
+    assert g.order is not None and int(deg.max()) > 500
     order = g.order.cpu().long()
     assert torch.equal(deg[order], torch.sort(deg, descending=True, stable=True).values)
     assert torch.equal(torch.sort(order).values, torch.arange(n))
