@@ -169,6 +169,24 @@ int big_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int6
                       int64_t num_rows, int64_t nc, int64_t bn, const int32_t* rowptr,
                       int64_t scale_cols, void* out, int64_t ldo, hipStream_t stream);
 
+// Persistent register-A bf16 kernels (gemm_stream.hip) for K in {256, 512}:
+// the forward at F_out = 256 and the dX GEMM at 256 | 512 output columns.
+// SLDM_STREAM_GEMM=0 disables them (falls back to the big-tile kernels).
+bool stream_gemm_enabled();
+bool stream_dense_fwd_ok(int64_t k0, int64_t K, int64_t nc, const void* a0, int64_t lda0,
+                         const void* a1, int64_t lda1, const void* w, const void* out,
+                         const void* xhat);
+bool stream_rowscale_ok(int64_t k, int64_t nc, const void* a, int64_t lda, const void* b,
+                        int64_t ldb, const void* out, int64_t ldo, int64_t scale_cols);
+int stream_dense_fwd(const void* a0, int64_t lda0, int64_t k0, const void* a1, int64_t lda1,
+                     int64_t k1, const void* w, int64_t num_rows, const float* bias,
+                     const float* gamma, const float* beta, float eps, float slope, float drop_p,
+                     uint64_t seed, int64_t row_off, void* out, void* xhat, float* rstd,
+                     hipStream_t stream);
+int stream_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int64_t ldb,
+                         int64_t num_rows, int64_t nc, const int32_t* rowptr, int64_t scale_cols,
+                         void* out, int64_t ldo, hipStream_t stream);
+
 }  // namespace sldm
 
 #define SLDM_REQUIRE(cond, ...)          \

@@ -651,6 +651,12 @@ extern "C" int sldm_sage_dense_fwd(int dtype, const void* a0, int64_t lda0, int6
   SLDM_REQUIRE(a0 && w && out && gamma && beta && (k1 == 0 || a1),
                "sldm_sage_dense_fwd: NULL argument");
   hipStream_t stream = sldm::as_stream(stream_);
+  if (dtype == SLDM_BF16 && sldm::stream_gemm_enabled() &&
+      sldm::stream_dense_fwd_ok(k0, k0 + k1, nc, a0, lda0, k1 ? a1 : a0, k1 ? lda1 : lda0, w,
+                                out, xhat))
+    return sldm::stream_dense_fwd(a0, lda0, k0, a1, lda1, k1, w, num_rows, bias, gamma, beta,
+                                  eps, negative_slope, drop_p, seed, row_off, out, xhat, rstd,
+                                  stream);
   if (dtype == SLDM_BF16 && sldm::big_gemm_enabled() && (nc == 128 || nc == 256) &&
       sldm::big_gemm_ok(k0, k0 + k1, nc, a0, lda0, k1 ? a1 : a0, k1 ? lda1 : lda0, w, k0 + k1,
                         nc))
@@ -686,6 +692,10 @@ extern "C" int sldm_gemm_nt_rowscale(int dtype, const void* a, int64_t lda, int6
   if (num_rows == 0) return SLDM_OK;
   SLDM_REQUIRE(a && b && out, "sldm_gemm_nt_rowscale: NULL argument");
   hipStream_t stream = sldm::as_stream(stream_);
+  if (dtype == SLDM_BF16 && sldm::stream_gemm_enabled() &&
+      sldm::stream_rowscale_ok(k, nc, a, lda, b, ldb, out, ldo, scale_cols))
+    return sldm::stream_gemm_rowscale(a, lda, k, b, ldb, num_rows, nc, rowptr, scale_cols, out,
+                                      ldo, stream);
   if (dtype == SLDM_BF16 && sldm::big_gemm_enabled() && nc % 128 == 0) {
     const int64_t bn = nc % 256 == 0 ? 256 : 128;
     if (sldm::big_gemm_ok(k, k, bn, a, lda, a, lda, b, ldb, ldo))

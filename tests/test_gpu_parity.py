@@ -522,3 +522,61 @@ def test_gemm_tn_large_split(dtype):
     ref = (dh.double().t() @ torch.cat([agg.double(), x.double()], 1)).float()
     s = ref.abs().max().item()
     torch.testing.assert_close(dw.cpu() / s, ref / s, atol=1e-5, rtol=1e-4)
+
+
+# ------------------------------------------- persistent stream kernels --
+# gemm_stream.hip serves bf16 K in {256, 512}: the forward at F_out = 256 and
+# the dX GEMM at 256 | 512 output columns.  Row counts cover one partial tile,
+# exact tiles, a ragged final tile and several tiles per persistent block
+# (70_001 rows = 274 forward tiles / 547 dX tiles on 256 blocks).
+STREAM_ROWS = [1, 255, 256, 257, 2000, 70_001]
+
+
+@pytest.mark.parametrize("m", STREAM_ROWS)
+@pytest.mark.parametrize("fi", [128, 256])
+def test_stream_dense_fwd_vs_torch_and_mask(m, fi):
+    from sldm_sage import ops
+    from sldm_sage.dense import weight_cat
+    fo, p, seed = 256, 0.25, 4242
+    gen = torch.Generator(device=DEV).manual_seed(m + fi)
+    agg, x = (torch.randn(m, fi, generator=gen, device=DEV).bfloat16() for _ in range(2))
+    wl, wr = (torch.randn(fo, fi, generator=gen, device=DEV) / fi ** 0.5 for _ in range(2))
+    bl, gam = (torch.randn(fo, generator=gen, device=DEV) for _ in range(2))
+    bet = torch.full((fo,), 6.0, device=DEV)            # y != 0: the kept mask is out != 0
+    wcat = weight_cat(wl, wr, torch.bfloat16)
+    out, xhat, rstd = ops.sage_dense_fwd(agg, x, wcat, bl, gam, bet, 1e-5, 0.1, p, seed, True)
+    h = agg.float() @ wcat[:, :fi].float().t() + bl + x.float() @ wcat[:, fi:].float().t()
+    mu = h.mean(1, keepdim=True)
+    rs = 1 / torch.sqrt(((h - mu) ** 2).mean(1, keepdim=True) + 1e-5)
+    xh = (h - mu) * rs
+    y = xh * gam + bet
+    # mask: the same counter hash post_fwd / post_bwd regenerate
+    ref_mask_out, _, _ = ops.post_fwd(torch.zeros(m, fo, device=DEV), None, torch.ones(fo, device=DEV),
+                                      torch.ones(fo, device=DEV), 1e-5, 0.1, p, seed,
+                                      torch.float32, False)
+    kept = out != 0
+    assert torch.equal(kept, ref_mask_out != 0)
+    z = torch.where(y > 0, y, 0.1 * y) / (1 - p)
+    torch.testing.assert_close(out.float()[kept], z[kept], atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(xhat.float(), xh, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(rstd, rs.squeeze(1), atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("m", STREAM_ROWS)
+@pytest.mark.parametrize("fi", [128, 256])
+def test_stream_gemm_rowscale_vs_torch(m, fi):
+    from sldm_sage import build_graph, ops
+    from sldm_sage.dense import weight_cat
+    from oracle.sage_ref import random_graph
+    fo = 256
+    ei, _ = random_graph(m, 3 * m + 1, 1, seed=m)
+    g = build_graph(ei.to(DEV), m)
+    gen = torch.Generator(device=DEV).manual_seed(m + fi)
+    dh = torch.randn(m, fo, generator=gen, device=DEV).bfloat16()
+    wl, wr = (torch.randn(fo, fi, generator=gen, device=DEV) for _ in range(2))
+    wt = weight_cat(wl, wr, torch.bfloat16).t().contiguous()          # [2 fi, fo]
+    out = ops.gemm_nt_rowscale(dh, wt, g.rowptr, fi)
+    ref = dh.float() @ wt.float().t()
+    deg = (g.rowptr[1:] - g.rowptr[:-1]).clamp(min=1).float()
+    ref[:, :fi] /= deg[:, None]
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=2e-2)
