@@ -114,8 +114,8 @@ inline int lanes_per_row(int64_t feat, int v) {
   return l;
 }
 
-// Counter-based dropout: u(seed, row, col) uniform in [0,1).  One 32-bit
-// integer hash (two v_mul_lo_u32) per element on top of a per-row key, so the
+// Counter-based dropout mask keyed by (seed, row, col): a per-row key, then
+// one 32-bit integer hash (two v_mul_lo_u32) per pair of columns, so the
 // backward regenerates the forward's mask exactly.
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16;
@@ -129,8 +129,34 @@ __device__ __forceinline__ uint32_t dropout_row_key(uint64_t seed, uint64_t row)
   return hash32((uint32_t)seed ^ hash32((uint32_t)(seed >> 32) ^ hash32((uint32_t)row) ^
                                         (uint32_t)(row >> 32) * 0x9E3779B9u));
 }
-__device__ __forceinline__ float dropout_uniform(uint32_t row_key, uint32_t col) {
-  return (float)(hash32(row_key + col * 0x9E3779B9u) >> 8) * (1.0f / 16777216.0f);
+// Two columns per hash: columns 2j and 2j+1 of a row take the low and high
+// 16 bits of hash32(row_key + j * golden); a column is kept iff its 16 bits
+// are >= thr = round(p * 2^16), i.e. p is quantised to 2^-16 (keep-rate error
+// <= 2^-17; the kept values are still scaled by the exact 1 / (1 - p)).
+__device__ __forceinline__ uint32_t dropout_threshold(float p) {
+  return p >= 1.f ? 65536u : (p <= 0.f ? 0u : (uint32_t)(p * 65536.f + 0.5f));
+}
+__device__ __forceinline__ bool dropout_keep(uint32_t row_key, uint32_t col, uint32_t thr) {
+  const uint32_t h = hash32(row_key + (col >> 1) * 0x9E3779B9u);
+  return ((col & 1u) ? (h >> 16) : (h & 0xFFFFu)) >= thr;
+}
+// Columns c, c+1 with c even: one hash.
+__device__ __forceinline__ void dropout_keep2(uint32_t row_key, uint32_t c_even, uint32_t thr,
+                                              bool& k0, bool& k1) {
+  const uint32_t h = hash32(row_key + (c_even >> 1) * 0x9E3779B9u);
+  k0 = (h & 0xFFFFu) >= thr;
+  k1 = (h >> 16) >= thr;
+}
+// V consecutive columns from f0 (a multiple of V): pairs share a hash.
+template <int V>
+__device__ __forceinline__ void dropout_keepv(uint32_t row_key, uint32_t f0, uint32_t thr,
+                                              bool (&keep)[V]) {
+  if constexpr (V == 1) {
+    keep[0] = dropout_keep(row_key, f0, thr);
+  } else {
+#pragma unroll
+    for (int k = 0; k < V; k += 2) dropout_keep2(row_key, f0 + k, thr, keep[k], keep[k + 1]);
+  }
 }
 
 // --------------------------------------------------- cross-lane reductions --

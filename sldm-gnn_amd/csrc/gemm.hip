@@ -327,8 +327,8 @@ __global__ __launch_bounds__(kBlock, 2) void gemm_nt_kernel(NtArgs<T> p) {
         const float y = xh[j] * p.gamma[c] + p.beta[c];
         float a = y > 0.f ? y : y * p.slope;
         if (p.drop_p > 0.f) {
-          const float u = sldm::dropout_uniform(rkey, (uint32_t)c);
-          a = (u >= p.drop_p) ? a * p.drop_scale : 0.f;
+          a = sldm::dropout_keep(rkey, (uint32_t)c, sldm::dropout_threshold(p.drop_p))
+                  ? a * p.drop_scale : 0.f;
         }
         z[j] = a;
       }

@@ -164,6 +164,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_big_kernel(BigArgs p) {
       for (int r = 0; r < 4; ++r) bvec[t][r] = p.bias ? p.bias[c + r] : 0.f;
     }
     const float inv_n = 1.0f / (float)p.Nc;
+    const uint32_t dthr = sldm::dropout_threshold(p.drop_p);
     float mean[4], rstdv[4];
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
@@ -215,16 +216,17 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_big_kernel(BigArgs p) {
       for (int t = 0; t < NT; ++t) {
         const int c = cbase + 16 * t;
         float xh[4], z[4];
+        bool keep[4] = {true, true, true, true};
+        if (p.drop_p > 0.f) {
+          sldm::dropout_keep2(rkey, (uint32_t)c, dthr, keep[0], keep[1]);
+          sldm::dropout_keep2(rkey, (uint32_t)c + 2, dthr, keep[2], keep[3]);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           xh[r] = (acc[m][t][r] + bvec[t][r] - mean[m]) * rstdv[m];
           const float y = xh[r] * gv[t][r] + bv[t][r];
-          float a = y > 0.f ? y : y * p.slope;
-          if (p.drop_p > 0.f) {
-            const float u = sldm::dropout_uniform(rkey, (uint32_t)(c + r));
-            a = (u >= p.drop_p) ? a * p.drop_scale : 0.f;
-          }
-          z[r] = a;
+          const float a = y > 0.f ? y : y * p.slope;
+          z[r] = keep[r] ? a * p.drop_scale : 0.f;
         }
         sldm::Vec<uint16_t, 4>::store(p.out + row * p.ldo + c, z);
         if (p.xhat) sldm::Vec<uint16_t, 4>::store(p.xhat + row * p.ldo + c, xh);

@@ -273,6 +273,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
     if constexpr (MODE == ST_LN) {
       char* stg = stage_base + wave * 16 * SROW;
       const float inv_n = 1.0f / 256.f;
+      const uint32_t dthr = sldm::dropout_threshold(p.drop_p);
       const int cq = 4 * q;
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
@@ -325,15 +326,16 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
             } else {
               const f4v gg = *reinterpret_cast<const f4v*>(prm + 256 + c);
               const f4v be = *reinterpret_cast<const f4v*>(prm + 512 + c);
+              bool keep[4] = {true, true, true, true};
+              if (p.drop_p > 0.f) {
+                sldm::dropout_keep2(rkey, (uint32_t)c, dthr, keep[0], keep[1]);
+                sldm::dropout_keep2(rkey, (uint32_t)c + 2, dthr, keep[2], keep[3]);
+              }
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const float y = acc[m][t][r] * gg[r] + be[r];
-                float a = y > 0.f ? y : y * p.slope;
-                if (p.drop_p > 0.f) {
-                  const float u = sldm::dropout_uniform(rkey, (uint32_t)(c + r));
-                  a = (u >= p.drop_p) ? a * p.drop_scale : 0.f;
-                }
-                v[r] = a;
+                const float a = y > 0.f ? y : y * p.slope;
+                v[r] = keep[r] ? a * p.drop_scale : 0.f;
               }
             }
             sldm::Vec<uint16_t, 4>::store(reinterpret_cast<uint16_t*>(stg + r16 * SROW + 2 * c),

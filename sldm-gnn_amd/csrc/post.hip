@@ -59,22 +59,23 @@ __global__ __launch_bounds__(kBlock) void post_fwd_kernel(
   if (!live) return;
   if (rstd_out && lane_in_row == 0) rstd_out[row] = rstd;
   const uint32_t rkey = sldm::dropout_row_key(seed, (uint64_t)(row + row_off));
+  const uint32_t dthr = sldm::dropout_threshold(drop_p);
 
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     if (!act[c]) continue;
     float xh[V], z[V];
+    bool keep[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) keep[k] = true;
+    if (drop_p > 0.0f) sldm::dropout_keepv<V>(rkey, (uint32_t)f0[c], dthr, keep);
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const int f = f0[c] + k;
       xh[k] = (v[c][k] - mean) * rstd;
       float y = xh[k] * gamma[f] + beta[f];
       float a = y > 0.0f ? y : y * slope;
-      if (drop_p > 0.0f) {
-        float u = sldm::dropout_uniform(rkey, (uint32_t)f);
-        a = (u >= drop_p) ? a * drop_scale : 0.0f;
-      }
-      z[k] = a;
+      z[k] = keep[k] ? a * drop_scale : 0.0f;
     }
     sldm::Vec<TO, V>::store(out + row * (int64_t)feat + f0[c], z);
     if (xhat_out) sldm::Vec<TO, V>::store(xhat_out + row * (int64_t)feat + f0[c], xh);
@@ -120,6 +121,7 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
     const int64_t r = live ? row : 0;
     const float rs = rstd[r];
     const uint32_t rkey = sldm::dropout_row_key(seed, (uint64_t)(r + row_off));
+    const uint32_t dthr = sldm::dropout_threshold(drop_p);
     float xh[NCH][V], gx[NCH][V], dy[NCH][V];
     float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll
@@ -128,17 +130,16 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
       sldm::Vec<T, V>::load(dout + r * (int64_t)feat + f0[c], go);
       sldm::Vec<T, V>::load(xhat + r * (int64_t)feat + f0[c], xh[c]);
       if (zout) sldm::Vec<T, V>::load(zout + r * (int64_t)feat + f0[c], zo);
+      bool kp[V];
+#pragma unroll
+      for (int k = 0; k < V; ++k) kp[k] = true;
+      if (drop_p > 0.0f) sldm::dropout_keepv<V>(rkey, (uint32_t)f0[c], dthr, kp);
 #pragma unroll
       for (int k = 0; k < V; ++k) {
         const int f = f0[c] + k;
         const float g = gamma[f];
-        float d = go[k];
-        bool keep = true;
-        if (drop_p > 0.0f) {
-          float u = sldm::dropout_uniform(rkey, (uint32_t)f);
-          keep = u >= drop_p;
-          d = keep ? d * drop_scale : 0.0f;
-        }
+        const bool keep = kp[k];
+        float d = keep ? go[k] * drop_scale : 0.0f;
         // Activation branch: from the saved output when given (sign(z) ==
         // sign(y) exactly, even with bf16 storage); else from y = xhat*g+b,
         // which a rounded xhat can flip where |y| is tiny.
