@@ -178,8 +178,17 @@ def main():
         g_in = gout[part.row_begin:part.row_end].contiguous()
         hf, hb = part.halo_rows()
         cross = float((part.fwd.col.long() >= part.num_rows).float().mean()) if part.fwd.num_edges else 0.0
+        def resident(split):
+            # fraction of own rows aggregated while the halo exchange is in flight
+            if split is None:
+                return 1.0
+            r, pnd = split.resident.rows.numel(), split.pending.rows.numel()
+            return round(r / max(r + pnd, 1), 4)
+
         dist_info = {"halo_rows_fwd_rank0": hf, "halo_rows_bwd_rank0": hb,
-                     "cross_partition_edge_fraction_rank0": round(cross, 4)}
+                     "cross_partition_edge_fraction_rank0": round(cross, 4),
+                     "overlap_resident_rows_fwd_rank0": resident(part.fwd_split),
+                     "overlap_resident_rows_bwd_rank0": resident(part.bwd_split)}
         del ei, x, gout
         torch.cuda.empty_cache()
 
@@ -238,14 +247,17 @@ def main():
         achieved = g["avg_bytes"] / (g["avg_ms"] * 1e-3) / 1e9
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "r1_c4_pmc_traffic.json")
-        if args.config == "c4" and os.path.exists(pmc):
+        if (args.config == "c4" and args.graph == "uniform" and world == 1
+                and os.path.exists(pmc)):
             # HBM bytes per launch of this kernel at this workload, from the
             # committed rocprofv3 PMC passes (2*FETCH_SIZE + WRITE_SIZE).
             with open(pmc) as fh:
                 traffic = int(json.load(fh)["gather_fwd_c4"]["hbm_bytes_per_launch"])
         roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
-                    traffic_unit="bytes/launch (PMC, profiles/r1_c4_pmc_traffic.json)",
+                    traffic_unit=("bytes/launch (PMC, profiles/r1_c4_pmc_traffic.json)"
+                                  if traffic is not None else
+                                  "no PMC pass committed for this workload"),
                     kernel="gather_rows_kernel (forward mean aggregation)",
                     avg_ms=round(g["avg_ms"], 4), launches=g["launches"],
                     bytes_per_launch=int(g["avg_bytes"]))

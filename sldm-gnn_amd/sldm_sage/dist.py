@@ -13,14 +13,15 @@ positions [0, n_own) are the rank's own rows, the rest are the remote rows it
 actually references, grouped by owner (sorted).  A halo *plan* per direction
 holds, for every peer, which of our rows it needs (send list) and how many of
 its rows we receive; the lists are exchanged once, at partition time.
-Per layer:
-  forward   buf = [x_own | all_to_all_v(x_own[send_idx])]      (RCCL)
-            agg = gather-mean over own in-edges from buf
+Per layer (RCCL ops are issued async and run on RCCL's stream):
+  forward   buf = [x_own | all_to_all_v(x_own[send_idx])]      (in flight)
+            agg = gather-mean, first over rows whose in-edges read only own
+                  rows, then (after the wait) over rows that read halo rows
             out = dense + LayerNorm + act + dropout on own rows
   backward  dh, [dAgg/deg | dx_root] on own rows
-            buf = [g_own | all_to_all_v(g_own[send_idx])]       (second plan)
-            dx  = dx_root + transpose gather over own out-edges from buf
-            weight grads: one bucketed all_reduce(SUM) per layer
+            buf = [g_own | all_to_all_v(g_own[send_idx])]       (in flight)
+            weight-grad GEMM + one bucketed all_reduce(SUM)      (in flight)
+            dx  = dx_root + transpose gather, halo-free rows first, then the rest
 Only referenced rows cross xGMI (on a uniform random graph with E/N = 10 and
 8 ranks that is ~71% of the remote rows; on a partition-local graph far
 fewer).  Each row's edges are summed in the same order as on one GPU and
@@ -53,10 +54,18 @@ class HipBackend:
         return rowptr, col, t_rowptr, t_col
 
     @staticmethod
-    def gather(x, rowptr, col, num_rows, mean, addend=None):
+    def gather(x, rowptr, col, num_rows, mean, addend=None, rows=None, out=None):
+        """Rows ``rows`` (a :class:`RowSubset`; all rows when None) of the CSR
+        gather, written into ``out`` (allocated when None)."""
         from . import ops
-        return ops.gather_rows(x, rowptr, col, num_rows, mean=mean, addend=addend,
-                               name="gather_fwd" if mean else "gather_bwd")
+        name = "gather_fwd" if mean else "gather_bwd"
+        if rows is None:
+            return ops.gather_rows(x, rowptr, col, num_rows, mean=mean, addend=addend, out=out,
+                                   name=name)
+        if out is None:
+            out = torch.empty(num_rows, x.size(1), dtype=x.dtype, device=x.device)
+        return ops.gather_rows(x, rowptr, col, rows.rows.numel(), mean=mean, addend=addend,
+                               out=out, name=name, order=rows.rows, edges=rows.edges)
 
     @staticmethod
     def pick_rows(x, rowptr, idx):
@@ -102,6 +111,43 @@ class HaloPlan:
 
 
 @dataclass
+class RowSubset:
+    rows: torch.Tensor            # int32 local row ids
+    edges: int                    # in-edges of those rows
+
+
+@dataclass
+class RowSplit:
+    """A partition graph's rows split by whether they read halo rows.
+
+    ``resident`` rows read only own rows, so they are aggregated while the
+    halo exchange is in flight; ``pending`` rows wait for it.  Each row is
+    still summed in CSR order by one kernel, so results are unchanged."""
+
+    resident: RowSubset
+    pending: RowSubset
+
+
+def _split_rows(g: SageGraph, n_own: int) -> RowSplit | None:
+    n = g.num_nodes
+    if n == 0 or g.num_edges == 0:
+        return None
+    dev = g.rowptr.device
+    deg = (g.rowptr[1:] - g.rowptr[:-1]).long()
+    row_of_edge = torch.repeat_interleave(torch.arange(n, device=dev), deg)
+    halo_edge = g.col[: g.num_edges].long() >= n_own
+    if not bool(halo_edge.any()):
+        return None
+    has_halo = torch.zeros(n, dtype=torch.bool, device=dev)
+    has_halo[row_of_edge[halo_edge]] = True
+    pend = has_halo.nonzero().squeeze(1)
+    res = (~has_halo).nonzero().squeeze(1)
+    pend_edges = int(deg[pend].sum())
+    return RowSplit(RowSubset(res.to(torch.int32), g.num_edges - pend_edges),
+                    RowSubset(pend.to(torch.int32), pend_edges))
+
+
+@dataclass
 class GraphPartition:
     """One rank's share of a graph (see module docstring)."""
 
@@ -115,6 +161,8 @@ class GraphPartition:
     bwd: SageGraph               # rows = own nodes, col = halo-buffer positions (destinations)
     fwd_plan: HaloPlan
     bwd_plan: HaloPlan
+    fwd_split: RowSplit | None = None   # overlap schedule of the forward gather
+    bwd_split: RowSplit | None = None   # ... and of the transpose gather
 
     @property
     def num_rows(self) -> int:
@@ -187,7 +235,23 @@ def partition_graph(edge_index: torch.Tensor, num_nodes: int, world: int, rank: 
     _, _, trp, tcol = backend.csr(fout, max(n_buf_b, 1), True)
     fwd = SageGraph(n, int(ein.size(1)), rp[: n + 1], col, None, None)
     bwd = SageGraph(n, int(eout.size(1)), trp[: n + 1], tcol, None, None)
-    return GraphPartition(rank, world, num_nodes, P, r0, r1, fwd, bwd, plan_f, plan_b)
+    return GraphPartition(rank, world, num_nodes, P, r0, r1, fwd, bwd, plan_f, plan_b,
+                          _split_rows(fwd, n), _split_rows(bwd, n))
+
+
+def _overlapped_gather(backend, buf, work, g: SageGraph, split: RowSplit | None, num_rows,
+                       mean, addend=None):
+    """The partition gather with the halo exchange ``work`` in flight: rows
+    that read only own rows first, then (after ``work.wait()``) the rest."""
+    if work is None or split is None:
+        if work is not None:
+            work.wait()
+        return backend.gather(buf, g.rowptr, g.col, num_rows, mean, addend=addend)
+    out = backend.gather(buf, g.rowptr, g.col, num_rows, mean, addend=addend,
+                         rows=split.resident)
+    work.wait()
+    return backend.gather(buf, g.rowptr, g.col, num_rows, mean, addend=addend,
+                          rows=split.pending, out=out)
 
 
 def _halo_buffer(x_own: torch.Tensor, plan: HaloPlan, backend, group, async_op=False):
@@ -214,8 +278,11 @@ class _DistLayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wl, bl, wr, gamma, beta, part: GraphPartition, group, backend,
                 slope, drop_p, seed, eps):
-        buf = _halo_buffer(x, part.fwd_plan, backend, group)
-        agg = backend.gather(buf, part.fwd.rowptr, part.fwd.col, part.num_rows, True)
+        # halo exchange on RCCL's stream; rows that read only own rows are
+        # aggregated meanwhile (buf[:n] is already the own block)
+        buf, work = _halo_buffer(x, part.fwd_plan, backend, group, async_op=True)
+        agg = _overlapped_gather(backend, buf, work, part.fwd, part.fwd_split, part.num_rows,
+                                 True)
         del buf
         save = any(ctx.needs_input_grad[:6])
         out, xhat, rstd = backend.layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p,
@@ -244,10 +311,8 @@ class _DistLayerFn(torch.autograd.Function):
         rwork = None
         if part.world > 1:
             rwork = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group, async_op=True)
-        if xwork is not None:
-            xwork.wait()
-        dx = be.gather(buf, part.bwd.rowptr, part.bwd.col, part.num_rows, False,
-                       addend=dx_r.contiguous())
+        dx = _overlapped_gather(be, buf, xwork, part.bwd, part.bwd_split, part.num_rows, False,
+                                addend=dx_r.contiguous())
         if rwork is not None:
             rwork.wait()
         dwl, dbl, dwr, dgamma, dbeta = (c.view_as(t) for c, t in zip(

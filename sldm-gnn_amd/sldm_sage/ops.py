@@ -126,10 +126,13 @@ def degree_order(rowptr: torch.Tensor) -> torch.Tensor:
 def gather_rows(x: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor, num_rows: int,
                 mean: bool, addend: torch.Tensor | None = None,
                 out: torch.Tensor | None = None, name: str = "gather",
-                order: torch.Tensor | None = None) -> torch.Tensor:
+                order: torch.Tensor | None = None, edges: int | None = None) -> torch.Tensor:
     """out[i] = (addend[i] +) sum_{k in row i} x[col[k]]  (/ max(1, deg_i) if mean).
 
-    ``order`` (optional) is a row schedule from :func:`degree_order`."""
+    ``order`` (optional) lists the rows to compute, slot s -> row order[s]
+    (``num_rows`` = len(order)): a schedule from :func:`degree_order`, or a
+    row subset (then ``out`` holds all rows and ``edges`` is the subset's
+    edge count, for the timing hook's byte accounting)."""
     dev = _require_gpu(x, rowptr, col, addend, out, order)
     if x.dim() != 2 or x.stride(1) != 1:
         x = x.contiguous()
@@ -143,7 +146,7 @@ def gather_rows(x: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor, num_ro
         return out
     E = col.numel()
     s = x.element_size()
-    bytes_alg = E * (4 + F * s) + (num_rows + 1) * 4 + num_rows * F * s * (2 if addend is not None else 1)
+    bytes_alg = (E if edges is None else edges) * (4 + F * s) + (num_rows + 1) * 4 + num_rows * F * s * (2 if addend is not None else 1)
     with _Timed(name, bytes_alg):
         _lib.check(_lib.load().sldm_gather_rows(
             dtype_code(x), x.data_ptr(), x.stride(0), rowptr.data_ptr(),

@@ -26,7 +26,18 @@ class CpuBackend:
         return rp, col, trp, tcol
 
     @staticmethod
-    def gather(x, rowptr, col, num_rows, mean, addend=None):
+    def gather(x, rowptr, col, num_rows, mean, addend=None, rows=None, out=None):
+        full = CpuBackend._gather_all(x, rowptr, col, num_rows, mean, addend)
+        if rows is None:
+            return full
+        if out is None:
+            out = torch.full_like(full, float("nan"))     # untouched rows stay visible
+        idx = rows.rows.long()
+        out[idx] = full[idx]
+        return out
+
+    @staticmethod
+    def _gather_all(x, rowptr, col, num_rows, mean, addend):
         rowptr = rowptr.long()
         base = rowptr[0]
         deg = rowptr[1:] - rowptr[:-1]
