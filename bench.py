@@ -163,81 +163,98 @@ def main():
 
     cfg = CONFIGS[args.config]
     n, e, f, L, dtype, desc = cfg
-    ei, x = make_graph(n, e, f, dtype, dev, kind=args.graph)
-    torch.manual_seed(0)
-    blk = SageBlock([f] * (L + 1), dropout=0.25, negative_slope=0.1).to(dev).train()
-    gout = torch.randn(n, f, device=dev, generator=torch.Generator(device=dev).manual_seed(2)
-                       ).to(dtype)
-
-    dist_info = {}
-    if use_dist:
-        from sldm_sage.dist import DistSageBlock, partition_graph
-        part = partition_graph(ei, n, world, rank)
-        model = DistSageBlock(blk, part)
-        x_in = x[part.row_begin:part.row_end].contiguous()
-        g_in = gout[part.row_begin:part.row_end].contiguous()
-        hf, hb = part.halo_rows()
-        cross = float((part.fwd.col.long() >= part.num_rows).float().mean()) if part.fwd.num_edges else 0.0
-        def resident(split):
-            # fraction of own rows aggregated while the halo exchange is in flight
-            if split is None:
-                return 1.0
-            r, pnd = split.resident.rows.numel(), split.pending.rows.numel()
-            return round(r / max(r + pnd, 1), 4)
-
-        dist_info = {"halo_rows_fwd_rank0": hf, "halo_rows_bwd_rank0": hb,
-                     "cross_partition_edge_fraction_rank0": round(cross, 4),
-                     "overlap_resident_rows_fwd_rank0": resident(part.fwd_split),
-                     "overlap_resident_rows_bwd_rank0": resident(part.bwd_split)}
-        del ei, x, gout
-        torch.cuda.empty_cache()
-
-        def step():
-            xr = x_in.detach().requires_grad_(True)
-            out = model(xr)
-            out.backward(g_in)
-            return out
-    else:
-        def step():
-            xr = x.detach().requires_grad_(True)
-            out = blk(xr, ei)
-            out.backward(gout)
-            return out
 
     def barrier():
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize(dev)
 
-    for _ in range(args.warmup):
-        blk.zero_grad(set_to_none=True)
-        step()
-    timer = KernelTimer()
-    barrier()
-    ops.set_timing_hook(timer)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        blk.zero_grad(set_to_none=True)
-        step()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    ops.set_timing_hook(None)
-    if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        elapsed = tt.item()
-    kern = timer.summary()
+    def run(kind, timed_kernels):
+        """Build the workload on graph ``kind``, warm up, time args.steps steps
+        (max over ranks).  Returns (elapsed_s, kernel summary, dist info, incl)."""
+        ei, x = make_graph(n, e, f, dtype, dev, kind=kind)
+        torch.manual_seed(0)
+        blk = SageBlock([f] * (L + 1), dropout=0.25, negative_slope=0.1).to(dev).train()
+        gout = torch.randn(n, f, device=dev, generator=torch.Generator(device=dev).manual_seed(2)
+                           ).to(dtype)
+        dist_info = {}
+        if use_dist:
+            from sldm_sage.dist import DistSageBlock, partition_graph
+            part = partition_graph(ei, n, world, rank)
+            model = DistSageBlock(blk, part)
+            x_in = x[part.row_begin:part.row_end].contiguous()
+            g_in = gout[part.row_begin:part.row_end].contiguous()
+            hf, hb = part.halo_rows()
+            cross = (float((part.fwd.col.long() >= part.num_rows).float().mean())
+                     if part.fwd.num_edges else 0.0)
 
-    # CSR-build-inclusive step (N=1: static-graph cache cleared once)
-    incl = None
-    if world == 1 and not use_dist:
-        graph_cache.clear()
+            def resident(split):
+                # fraction of own rows aggregated while the halo exchange is in flight
+                if split is None:
+                    return 1.0
+                r, pnd = split.resident.rows.numel(), split.pending.rows.numel()
+                return round(r / max(r + pnd, 1), 4)
+
+            dist_info = {"halo_rows_fwd_rank0": hf, "halo_rows_bwd_rank0": hb,
+                         "cross_partition_edge_fraction_rank0": round(cross, 4),
+                         "overlap_resident_rows_fwd_rank0": resident(part.fwd_split),
+                         "overlap_resident_rows_bwd_rank0": resident(part.bwd_split)}
+            del ei, x, gout
+            torch.cuda.empty_cache()
+
+            def step():
+                xr = x_in.detach().requires_grad_(True)
+                out = model(xr)
+                out.backward(g_in)
+                return out
+        else:
+            def step():
+                xr = x.detach().requires_grad_(True)
+                out = blk(xr, ei)
+                out.backward(gout)
+                return out
+
+        for _ in range(args.warmup):
+            blk.zero_grad(set_to_none=True)
+            step()
+        timer = KernelTimer()
         barrier()
-        t1 = time.perf_counter()
-        blk.zero_grad(set_to_none=True)
-        step()
+        if timed_kernels:
+            ops.set_timing_hook(timer)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            blk.zero_grad(set_to_none=True)
+            step()
         barrier()
-        incl = e * L / (time.perf_counter() - t1)
+        elapsed = time.perf_counter() - t0
+        ops.set_timing_hook(None)
+        if world > 1:
+            tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+            torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+            elapsed = tt.item()
+
+        # CSR-build-inclusive step (N=1: static-graph cache cleared once)
+        incl = None
+        if world == 1 and not use_dist:
+            graph_cache.clear()
+            barrier()
+            t1 = time.perf_counter()
+            blk.zero_grad(set_to_none=True)
+            step()
+            barrier()
+            incl = e * L / (time.perf_counter() - t1)
+        return elapsed, timer.summary(), dist_info, incl
+
+    elapsed, kern, dist_info, incl = run(args.graph, True)
+    variant = None
+    if world > 1 and args.graph == "uniform":
+        # SURVEY.md §8d C4: also the locality-structured variant (block-community
+        # graph, cut fraction stated) -- the regime where the exchange overlaps.
+        torch.cuda.empty_cache()
+        v_el, _, v_info, _ = run("local", False)
+        variant = dict(graph="local", value=round(e * L * args.steps / v_el, 1),
+                       ms_per_step=round(v_el / args.steps * 1e3, 3), **v_info)
+        torch.cuda.empty_cache()
 
     ms = elapsed / args.steps * 1e3
     value = e * L * args.steps / elapsed
@@ -293,6 +310,8 @@ def main():
             "kernels": kernels,
             "cpu_baseline": base,
         }
+        if variant is not None:
+            line["locality_variant"] = variant
         print(json.dumps(line), flush=True)
     if use_dist:
         torch.distributed.destroy_process_group()
