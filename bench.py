@@ -10,9 +10,11 @@ resident in HBM before the timed region; the CSR is built on the first
 (warm-up) call and cached on the edge_index tensor, as for any static graph
 (``value_incl_csr_build`` re-times one step with the cache cleared).
 
-N > 1 (torchrun, one rank per GPU, RCCL): the graph's destination rows are
-partitioned across ranks (sldm_sage.dist), halo rows of x are exchanged with
-an all-gather per layer; ``scaling`` is "strong" (the graph is fixed).
+N > 1 (torchrun, one rank per GPU, RCCL): the graph is partitioned across
+ranks (sldm_sage.dist.plan_partition, ``--strategy``): destination rows with a
+halo all-to-all-v per layer, or feature slices with balanced layout
+all-to-alls, whichever has the lower modelled time for the graph at hand;
+``scaling`` is "strong" (the graph is fixed).
 
 The JSON line also carries ``roofline`` for the dominant kernel (the CSR
 gather-mean: the SageBlock scatter-add), measured with HIP events around
@@ -127,6 +129,12 @@ def cpu_baseline(cfg, threads):
                 ms_per_step=t * 1e3)
 
 
+def _parallelism(strategy, world):
+    if strategy == "feature":
+        return f"feature-sliced x{world} (all rows, F/{world} columns per rank), RCCL all-to-all"
+    return f"dst-partition x{world}, RCCL halo all-to-all"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -140,6 +148,9 @@ def main():
                          "in-degrees (default for c5)")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the partitioned (multi-GPU) path even on one GPU")
+    ap.add_argument("--strategy", default="auto", choices=["auto", "halo", "feature"],
+                    help="multi-GPU partition: destination rows + halo exchange, feature "
+                         "slices + layout all-to-alls, or the lower modelled time (default)")
     args = ap.parse_args()
 
     if args.graph is None:
@@ -179,26 +190,36 @@ def main():
                            ).to(dtype)
         dist_info = {}
         if use_dist:
-            from sldm_sage.dist import DistSageBlock, partition_graph
-            part = partition_graph(ei, n, world, rank)
+            from sldm_sage.dist import DistSageBlock, plan_partition
+            part, plan = plan_partition(ei, n, world, rank, f, x.element_size(),
+                                        strategy=args.strategy)
             model = DistSageBlock(blk, part)
             x_in = x[part.row_begin:part.row_end].contiguous()
             g_in = gout[part.row_begin:part.row_end].contiguous()
-            hf, hb = part.halo_rows()
-            cross = (float((part.fwd.col.long() >= part.num_rows).float().mean())
-                     if part.fwd.num_edges else 0.0)
+            dist_info = {"strategy": plan["strategy"],
+                         "exchange_bytes_per_layer_rank0":
+                             part.exchange_bytes_per_layer(f, x.element_size())}
+            for k in ("halo_s", "feature_s"):
+                if k in plan:
+                    dist_info[f"model_{k[:-2]}_ms_per_layer"] = round(plan[k] * 1e3, 3)
+            if plan["strategy"] == "halo":
+                hf, hb = part.halo_rows()
+                cross = (float((part.fwd.col.long() >= part.num_rows).float().mean())
+                         if part.fwd.num_edges else 0.0)
 
-            def resident(split):
-                # fraction of own rows aggregated while the halo exchange is in flight
-                if split is None:
-                    return 1.0
-                r, pnd = split.resident.rows.numel(), split.pending.rows.numel()
-                return round(r / max(r + pnd, 1), 4)
+                def resident(split):
+                    # fraction of own rows aggregated while the halo exchange is in flight
+                    if split is None:
+                        return 1.0
+                    r, pnd = split.resident.rows.numel(), split.pending.rows.numel()
+                    return round(r / max(r + pnd, 1), 4)
 
-            dist_info = {"halo_rows_fwd_rank0": hf, "halo_rows_bwd_rank0": hb,
-                         "cross_partition_edge_fraction_rank0": round(cross, 4),
-                         "overlap_resident_rows_fwd_rank0": resident(part.fwd_split),
-                         "overlap_resident_rows_bwd_rank0": resident(part.bwd_split)}
+                dist_info.update({"halo_rows_fwd_rank0": hf, "halo_rows_bwd_rank0": hb,
+                                  "cross_partition_edge_fraction_rank0": round(cross, 4),
+                                  "overlap_resident_rows_fwd_rank0": resident(part.fwd_split),
+                                  "overlap_resident_rows_bwd_rank0": resident(part.bwd_split)})
+            else:
+                dist_info["chunks"] = part.num_chunks
             del ei, x, gout
             torch.cuda.empty_cache()
 
@@ -303,7 +324,7 @@ def main():
                      }[args.graph] + ", x~N(0,1), random-init weights)",
             "config": {"workload": desc, "graph": args.graph, "nodes": n, "edges": e, "feat": f,
                        "layers": L, "dropout": 0.25, "negative_slope": 0.1,
-                       "parallelism": (f"dst-partition x{world}, RCCL halo all-to-all"
+                       "parallelism": (_parallelism(dist_info.get("strategy"), world)
                                        if use_dist else "single"), **dist_info},
             "value_incl_csr_build": round(incl, 1) if incl else None,
             "roofline": roof,

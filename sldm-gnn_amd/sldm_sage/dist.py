@@ -27,6 +27,26 @@ Only referenced rows cross xGMI (on a uniform random graph with E/N = 10 and
 fewer).  Each row's edges are summed in the same order as on one GPU and
 dropout keys use global row ids, so W ranks reproduce the single-GPU result.
 
+A second strategy, *feature slicing* (:func:`partition_features`), serves
+graphs where any row partition cuts nearly every edge (uniform random graphs:
+the halo is ~71% of all rows at W = 8 and ~99% at W = 2).  Every rank keeps
+the whole graph's CSR and aggregates ALL rows over its own slice of the
+feature columns, so the gathers need no halo; the dense part stays on the
+rank's row block, and layouts are switched by balanced all-to-alls:
+  forward   x_cols = row->col(x_own)                   [N, F/W]
+            agg_cols = gather-mean(x_cols)             all rows, own columns
+            agg_own  = col->row(agg_cols)              [P, F]
+            out = dense + LayerNorm + act + dropout on own rows
+  backward  dh, [g = dAgg/deg | dx_root] on own rows
+            g_cols = row->col(g)       (in flight with the weight-grad GEMM)
+            dx = dx_root + col->row(transpose-gather(g_cols))
+Per layer a rank moves 4 x (W-1)/W^2 x N x F x s bytes, against
+2 x halo x F x s for the row partition (C4 at W = 8: 2.2 GB vs 6.4 GB), the
+load is balanced by construction (power-law in-degrees included) and each
+element is still summed in CSR order (fp32: bit-identical to one GPU; bf16:
+the backward's two-term add rounds once more).  :func:`plan_partition`
+picks the strategy with the lower modelled time.
+
 The per-rank compute goes through a backend object (default: the HIP ops);
 the CPU tests plug a plain-torch backend in to run the same protocol over
 gloo.
@@ -54,14 +74,15 @@ class HipBackend:
         return rowptr, col, t_rowptr, t_col
 
     @staticmethod
-    def gather(x, rowptr, col, num_rows, mean, addend=None, rows=None, out=None):
+    def gather(x, rowptr, col, num_rows, mean, addend=None, rows=None, out=None, edges=None):
         """Rows ``rows`` (a :class:`RowSubset`; all rows when None) of the CSR
-        gather, written into ``out`` (allocated when None)."""
+        gather, written into ``out`` (allocated when None).  ``edges``: the
+        edge count of a rowptr window (byte accounting only)."""
         from . import ops
         name = "gather_fwd" if mean else "gather_bwd"
         if rows is None:
             return ops.gather_rows(x, rowptr, col, num_rows, mean=mean, addend=addend, out=out,
-                                   name=name)
+                                   name=name, edges=edges)
         if out is None:
             out = torch.empty(num_rows, x.size(1), dtype=x.dtype, device=x.device)
         return ops.gather_rows(x, rowptr, col, rows.rows.numel(), mean=mean, addend=addend,
@@ -172,6 +193,10 @@ class GraphPartition:
         """(rows received in the forward exchange, in the backward exchange)."""
         return self.fwd_plan.num_recv, self.bwd_plan.num_recv
 
+    def exchange_bytes_per_layer(self, feat: int, elem: int) -> int:
+        """Bytes this rank sends per layer (forward x rows + backward dAgg rows)."""
+        return (sum(self.fwd_plan.send_counts) + sum(self.bwd_plan.send_counts)) * feat * elem
+
 
 def _exchange_counts(counts: list[int], device, group) -> list[int]:
     world = len(counts)
@@ -274,6 +299,262 @@ def _halo_buffer(x_own: torch.Tensor, plan: HaloPlan, backend, group, async_op=F
     return (buf, work) if async_op else buf
 
 
+# ---------------------------------------------------------------------------
+# Feature slicing (module docstring, second strategy)
+# ---------------------------------------------------------------------------
+def _even_split(n: int, parts: int, align: int = 1) -> list[int]:
+    """``parts`` sizes summing to n, as equal as possible in units of ``align``."""
+    units, tail = divmod(n, align)
+    base, rem = divmod(units, parts)
+    sizes = [(base + (i < rem)) * align for i in range(parts)]
+    sizes[-1] += tail
+    return sizes
+
+
+@dataclass
+class FeaturePartition:
+    """One rank's view of a feature-sliced graph.
+
+    Node rows are relabelled into a *chunk-major* order pi: for chunk j of K,
+    for rank q in order, rank q's j-th sub-range of its own rows.  Then the
+    rows of one chunk are contiguous in every column-sliced buffer and, inside
+    the chunk, grouped by owning rank -- each chunk's layout switch is one
+    balanced all-to-all straight out of / into those buffers.  The CSR pair is
+    built over pi-labels (sources and destinations), stable, so each row's
+    edges keep their original order."""
+
+    rank: int
+    world: int
+    num_nodes: int
+    rows_per_rank: int
+    row_begin: int
+    row_end: int
+    graph: SageGraph                  # full graph, pi-labelled, with transpose
+    own_rowptr: torch.Tensor          # int32 [n_own+1]: in-degree prefix of own rows (natural order)
+    chunk_rows: list[list[int]]       # [K][W]: rows of rank q in chunk j
+    chunk_start: list[int]            # [K+1]: pi-row offset of chunk j
+    chunk_edges: list[int]            # [K]: in-edges of chunk j's rows
+    chunk_t_edges: list[int]          # [K]: out-edges of chunk j's rows
+    own_chunk: list[int]              # [K+1]: own-row offsets of the chunks
+
+    @property
+    def num_rows(self) -> int:
+        return self.row_end - self.row_begin
+
+    @property
+    def num_chunks(self) -> int:
+        return len(self.chunk_rows)
+
+    def col_sizes(self, feat: int) -> list[int]:
+        """Column slice widths of a ``feat``-wide layer, one per rank (16-B
+        multiples where F allows: whole vectors per lane in the gather)."""
+        align = 8 if feat >= 8 * self.world else 1
+        return _even_split(feat, self.world, align)
+
+    def exchange_bytes_per_layer(self, feat: int, elem: int) -> int:
+        """Bytes this rank sends per layer (fwd + bwd, 4 layout switches)."""
+        cs = self.col_sizes(feat)
+        own = self.num_rows
+        return 4 * sum(own * cs[c] for c in range(self.world) if c != self.rank) * elem
+
+
+def _chunk_bounds(n_own: int, chunks: int) -> list[int]:
+    return [(j * n_own) // chunks for j in range(chunks + 1)]
+
+
+def partition_features(edge_index: torch.Tensor, num_nodes: int, world: int, rank: int,
+                       backend=HipBackend, chunks: int = 4) -> FeaturePartition:
+    """Feature-sliced partition (no collective: every rank holds edge_index)."""
+    P = (num_nodes + world - 1) // world
+    dev = edge_index.device
+    begins = [min(q * P, num_nodes) for q in range(world)]
+    ends = [min((q + 1) * P, num_nodes) for q in range(world)]
+    k = max(1, min(chunks, max(e - b for b, e in zip(begins, ends))))
+    bounds = [_chunk_bounds(e - b, k) for b, e in zip(begins, ends)]
+    chunk_rows = [[bounds[q][j + 1] - bounds[q][j] for q in range(world)] for j in range(k)]
+    chunk_start = [0]
+    for j in range(k):
+        chunk_start.append(chunk_start[-1] + sum(chunk_rows[j]))
+    # pi: natural id -> chunk-major id, built piecewise
+    pi = torch.empty(num_nodes, dtype=torch.int64, device=dev)
+    pos = 0
+    for j in range(k):
+        for q in range(world):
+            a, b = begins[q] + bounds[q][j], begins[q] + bounds[q][j + 1]
+            pi[a:b] = torch.arange(pos, pos + b - a, device=dev)
+            pos += b - a
+    ei = torch.stack([pi[edge_index[0].long()], pi[edge_index[1].long()]]) \
+        if edge_index.numel() else edge_index.long()
+    rp, col, trp, tcol = backend.csr(ei, max(num_nodes, 1), True)
+    g = SageGraph(num_nodes, int(edge_index.size(1)), rp, col, trp, tcol)
+    deg_rp = rp.long()
+    t_rp = trp.long()
+    chunk_edges = [int(deg_rp[chunk_start[j + 1]] - deg_rp[chunk_start[j]]) for j in range(k)]
+    chunk_t_edges = [int(t_rp[chunk_start[j + 1]] - t_rp[chunk_start[j]]) for j in range(k)]
+    r0, r1 = begins[rank], ends[rank]
+    # own rows' in-degrees in natural order (1/deg of the bwd-data GEMM)
+    own_pi = pi[r0:r1]
+    own_deg = (deg_rp[own_pi + 1] - deg_rp[own_pi]).to(torch.int32)
+    own_rowptr = torch.zeros(r1 - r0 + 1, dtype=torch.int32, device=dev)
+    if r1 > r0:
+        own_rowptr[1:] = torch.cumsum(own_deg, 0).to(torch.int32)
+    return FeaturePartition(rank, world, num_nodes, P, r0, r1, g, own_rowptr, chunk_rows,
+                            chunk_start, chunk_edges, chunk_t_edges, bounds[rank])
+
+
+def _a2a(out, inp, out_splits, in_splits, group):
+    return dist.all_to_all_single(out, inp, output_split_sizes=out_splits,
+                                  input_split_sizes=in_splits, group=group, async_op=True)
+
+
+def _rows_to_cols(part: FeaturePartition, src: torch.Tensor, j: int, dst_cols: torch.Tensor,
+                  group):
+    """Chunk j of this rank's rows of ``src`` [n_own, F] -> rows
+    [chunk_start[j], chunk_start[j+1]) of the column-sliced ``dst_cols``
+    [N, F_r] on every rank.  Returns (work, keep-alive)."""
+    W, r = part.world, part.rank
+    a, b = part.own_chunk[j], part.own_chunk[j + 1]
+    cs = part.col_sizes(src.size(1))
+    if W == 1:
+        dst_cols[part.chunk_start[j]: part.chunk_start[j + 1]].copy_(src[a:b])
+        return None, None
+    rows = b - a
+    if all(c == cs[0] for c in cs):
+        send = src[a:b].reshape(rows, W, cs[0]).transpose(0, 1).contiguous()
+    else:
+        send = torch.cat([src[a:b, sum(cs[:c]): sum(cs[:c + 1])].reshape(-1)
+                          for c in range(W)]) if rows else src.new_empty(0)
+    recv = dst_cols[part.chunk_start[j]: part.chunk_start[j + 1]]
+    work = _a2a(recv.view(-1), send.view(-1), [n * cs[r] for n in part.chunk_rows[j]],
+                [rows * c for c in cs], group)
+    return work, send
+
+
+def _cols_to_rows(part: FeaturePartition, src_cols: torch.Tensor, j: int, feat: int, group):
+    """Rows [chunk_start[j], chunk_start[j+1]) of the column-sliced ``src_cols``
+    -> this rank's chunk-j rows, all columns, as (work, recv, sizes); finish
+    with :func:`_cols_to_rows_finish`."""
+    W, r = part.world, part.rank
+    cs = part.col_sizes(feat)
+    s0, s1 = part.chunk_start[j], part.chunk_start[j + 1]
+    rows = part.own_chunk[j + 1] - part.own_chunk[j]
+    if W == 1:
+        return None, src_cols[s0:s1], cs
+    recv = src_cols.new_empty(rows * feat)
+    work = _a2a(recv, src_cols[s0:s1].reshape(-1), [rows * c for c in cs],
+                [n * cs[r] for n in part.chunk_rows[j]], group)
+    return work, recv, cs
+
+
+def _cols_to_rows_finish(part, recv, cs, rows, out_rows):
+    """Interleave the per-rank column blocks of ``recv`` into ``out_rows`` [rows, F]."""
+    if part.world == 1:
+        out_rows.copy_(recv)
+        return
+    if all(c == cs[0] for c in cs):
+        out_rows.view(rows, part.world, cs[0]).copy_(
+            recv.view(part.world, rows, cs[0]).transpose(0, 1))
+        return
+    off, col = 0, 0
+    for c in cs:
+        out_rows[:, col:col + c].copy_(recv[off: off + rows * c].view(rows, c))
+        off += rows * c
+        col += c
+
+
+def _feat_gather(backend, src_cols, rowptr, col, part, j, mean, out_cols, edges):
+    s0, s1 = part.chunk_start[j], part.chunk_start[j + 1]
+    if s1 > s0 and src_cols.size(1):
+        backend.gather(src_cols, rowptr[s0: s1 + 1], col, s1 - s0, mean,
+                       out=out_cols[s0:s1], edges=edges)
+
+
+def _feat_aggregate_to_rows(backend, part, src_cols, rowptr, col, mean, feat, chunk_edges,
+                            group):
+    """Aggregate all rows over this rank's columns, chunk by chunk, and bring
+    each finished chunk back to row layout while the next chunk is gathered."""
+    out_cols = src_cols.new_empty(part.num_nodes, src_cols.size(1))
+    out_rows = src_cols.new_empty(part.num_rows, feat)
+    pending = []
+    for j in range(part.num_chunks):
+        _feat_gather(backend, src_cols, rowptr, col, part, j, mean, out_cols, chunk_edges[j])
+        pending.append((j,) + _cols_to_rows(part, out_cols, j, feat, group))
+    for j, work, recv, cs in pending:
+        if work is not None:
+            work.wait()
+        a, b = part.own_chunk[j], part.own_chunk[j + 1]
+        _cols_to_rows_finish(part, recv, cs, b - a, out_rows[a:b])
+    return out_rows
+
+
+def _feat_rows_to_cols(part, x_rows, group):
+    """Column-sliced copy [N, F_r] of the row-partitioned ``x_rows``; returns
+    (buffer, works) -- wait on every work before reading the buffer."""
+    cs = part.col_sizes(x_rows.size(1))
+    buf = x_rows.new_empty(part.num_nodes, cs[part.rank])
+    works = []
+    for j in range(part.num_chunks):
+        w, keep = _rows_to_cols(part, x_rows, j, buf, group)
+        if w is not None:
+            works.append((w, keep))
+    return buf, works
+
+
+def _wait_all(works):
+    for w, _ in works:
+        w.wait()
+
+
+class _FeatLayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, wl, bl, wr, gamma, beta, part: FeaturePartition, group, backend,
+                slope, drop_p, seed, eps):
+        g = part.graph
+        F = x.size(1)
+        x_cols, works = _feat_rows_to_cols(part, x, group)
+        _wait_all(works)
+        agg = _feat_aggregate_to_rows(backend, part, x_cols, g.rowptr, g.col, True, F,
+                                      part.chunk_edges, group)
+        del x_cols
+        save = any(ctx.needs_input_grad[:6])
+        out, xhat, rstd = backend.layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p,
+                                            seed, save, part.row_begin)
+        if save:
+            ctx.save_for_backward(x, agg, xhat, rstd, wl, wr, gamma, beta, out)
+            ctx.part, ctx.group, ctx.backend = part, group, backend
+            ctx.cfg = (slope, drop_p, seed)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, agg, xhat, rstd, wl, wr, gamma, beta, out = ctx.saved_tensors
+        part, group, be = ctx.part, ctx.group, ctx.backend
+        slope, drop_p, seed = ctx.cfg
+        gr = part.graph
+        F = x.size(1)
+        dh, dgamma, dbeta, dbl = be.post_bwd(dout.contiguous(), xhat, rstd, gamma, beta, slope,
+                                             drop_p, seed, out, part.row_begin)
+        g, dx_r = be.bwd_data(dh, wl, wr, part.own_rowptr)
+        # dAgg/deg to column layout (RCCL stream) while the weight-grad GEMM runs
+        g_cols, works = _feat_rows_to_cols(part, g, group)
+        dwl, dwr = be.bwd_weight(dh, agg, x)
+        grads = (dwl, dbl, dwr, dgamma, dbeta)
+        flat = torch.cat([t.reshape(-1).float() for t in grads])
+        rwork = None
+        if part.world > 1:
+            rwork = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group, async_op=True)
+        _wait_all(works)
+        dxa = _feat_aggregate_to_rows(be, part, g_cols, gr.t_rowptr, gr.t_col, False, F,
+                                      part.chunk_t_edges, group)
+        dx = dx_r + dxa
+        if rwork is not None:
+            rwork.wait()
+        dwl, dbl, dwr, dgamma, dbeta = (c.view_as(t) for c, t in zip(
+            torch.split(flat, [t.numel() for t in grads]), grads))
+        return (dx, dwl.to(wl.dtype), dbl.to(wl.dtype), dwr.to(wr.dtype), dgamma.to(gamma.dtype),
+                dbeta.to(beta.dtype), None, None, None, None, None, None, None)
+
+
 class _DistLayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wl, bl, wr, gamma, beta, part: GraphPartition, group, backend,
@@ -343,14 +624,95 @@ class DistSageBlock(nn.Module):
                 for p in block.parameters():
                     dist.broadcast(p.data, src=0, group=group)
 
+    @property
+    def strategy(self) -> str:
+        return "feature" if isinstance(self.part, FeaturePartition) else "halo"
+
     def forward(self, x_local: torch.Tensor) -> torch.Tensor:
         from .sageblock import _act_slope, _drop_p, _new_seed
+        fn = _FeatLayerFn if isinstance(self.part, FeaturePartition) else _DistLayerFn
         x = x_local.contiguous()
         for conv, post in zip(self.block.convs, self.block.posts):
             ln, act, drop = post[0], post[1], post[2]
             p = _drop_p(drop)
             seed = _new_seed() if p > 0 else 0
-            x = _DistLayerFn.apply(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight,
+            x = fn.apply(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight,
                                    ln.weight, ln.bias, self.part, self.group, self.backend,
                                    _act_slope(act), p, seed, float(ln.eps))
         return x
+
+
+# ---------------------------------------------------------------------------
+# Strategy planner
+# ---------------------------------------------------------------------------
+# Cost-model constants (MI355X, measured on one GPU):
+#   gather rate by gathered row width, uniform random rows of a multi-GB
+#   table (tools/gather_probe.py, profiles/r1_gather_probe.txt);
+#   xGMI: one link per peer, ~50 GB/s achieved per direction (conservative
+#   share of the 76.8 GB/s per-direction link rate).
+_GATHER_TBPS = ((64, 3.7e12), (128, 5.5e12), (256, 5.3e12), (512, 5.7e12), (1 << 30, 5.2e12))
+_LINK_BPS = 50e9
+
+
+def _gather_rate(row_bytes: int) -> float:
+    for limit, rate in _GATHER_TBPS:
+        if row_bytes <= limit:
+            return rate
+    return _GATHER_TBPS[-1][1]
+
+
+def _remote_unique(ids: torch.Tensor, r0: int, r1: int) -> int:
+    if ids.numel() == 0:
+        return 0
+    u = torch.unique(ids)
+    return int(((u < r0) | (u >= r1)).sum())
+
+
+def estimate_strategies(edge_index: torch.Tensor, num_nodes: int, world: int, rank: int,
+                        feat: int, elem: int, group=None) -> dict:
+    """Modelled per-layer time (s) of the halo and feature-sliced strategies,
+    max over ranks (collective over ``group`` when world > 1)."""
+    P = (num_nodes + world - 1) // world
+    r0, r1 = min(rank * P, num_nodes), min((rank + 1) * P, num_nodes)
+    src, dst = edge_index[0], edge_index[1]
+    in_mask = (dst >= r0) & (dst < r1)
+    out_mask = (src >= r0) & (src < r1)
+    halo_f = _remote_unique(src[in_mask], r0, r1)
+    halo_b = _remote_unique(dst[out_mask], r0, r1)
+    e_in, e_out = int(in_mask.sum()), int(out_mask.sum())
+    link = max(world - 1, 1) * _LINK_BPS
+    row = feat * elem
+    halo_t = ((halo_f + halo_b) * row / link
+              + (e_in + e_out) * (row + 4) / _gather_rate(row))
+    fc = max(1, feat // world)
+    e = int(edge_index.size(1))
+    feat_t = (4 * (world - 1) * (r1 - r0) * fc * elem / link
+              + 2 * e * (fc * elem + 4) / _gather_rate(fc * elem))
+    v = torch.tensor([halo_t, feat_t, float(halo_f), float(halo_b)], dtype=torch.float64,
+                     device=edge_index.device)
+    if world > 1:
+        dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
+    halo_t, feat_t, hf, hb = v.tolist()
+    return {"halo_s": halo_t, "feature_s": feat_t, "halo_rows_fwd_max": int(hf),
+            "halo_rows_bwd_max": int(hb)}
+
+
+def plan_partition(edge_index: torch.Tensor, num_nodes: int, world: int, rank: int,
+                   feat: int, elem: int, strategy: str = "auto", backend=HipBackend,
+                   group=None, chunks: int = 4):
+    """Partition with ``strategy`` in {"auto", "halo", "feature"}; "auto" takes
+    the lower modelled time of :func:`estimate_strategies` (every rank gets the
+    same answer: the estimate is max-reduced).  Returns (partition, info)."""
+    info = {}
+    if strategy == "auto":
+        if world == 1:
+            strategy = "halo"
+        else:
+            info = estimate_strategies(edge_index, num_nodes, world, rank, feat, elem, group)
+            strategy = "feature" if info["feature_s"] < info["halo_s"] else "halo"
+    info["strategy"] = strategy
+    if strategy == "feature":
+        return partition_features(edge_index, num_nodes, world, rank, backend, chunks), info
+    if strategy == "halo":
+        return partition_graph(edge_index, num_nodes, world, rank, backend, group), info
+    raise ValueError(f"unknown partition strategy {strategy!r} (auto, halo, feature)")

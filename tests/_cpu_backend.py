@@ -26,9 +26,12 @@ class CpuBackend:
         return rp, col, trp, tcol
 
     @staticmethod
-    def gather(x, rowptr, col, num_rows, mean, addend=None, rows=None, out=None):
+    def gather(x, rowptr, col, num_rows, mean, addend=None, rows=None, out=None, edges=None):
         full = CpuBackend._gather_all(x, rowptr, col, num_rows, mean, addend)
         if rows is None:
+            if out is not None:
+                out.copy_(full)
+                return out
             return full
         if out is None:
             out = torch.full_like(full, float("nan"))     # untouched rows stay visible

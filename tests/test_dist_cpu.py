@@ -1,8 +1,9 @@
-"""Multi-rank protocol of sldm_sage.dist over gloo on CPU (world sizes 2 and 3).
+"""Multi-rank protocol of sldm_sage.dist over gloo on CPU (world sizes 2-4).
 
-Each rank runs DistSageBlock on its destination-row partition (per-rank
-compute from the test's plain-torch backend) and must reproduce the oracle's
-full-graph output rows, input-gradient rows and the full parameter gradients.
+Each rank runs DistSageBlock on its partition -- destination rows + halo
+exchange, or feature slices + layout all-to-alls -- (per-rank compute from
+the test's plain-torch backend) and must reproduce the oracle's full-graph
+output rows, input-gradient rows and the full parameter gradients.
 """
 from __future__ import annotations
 
@@ -23,7 +24,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, hdims, n, e, q):
+def _worker(rank, world, port, hdims, n, e, q, strategy="halo", chunks=4):
     sys.path[:0] = [HERE, os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "sldm-gnn_amd")]
     import torch.distributed as dist
 
@@ -31,7 +32,7 @@ def _worker(rank, world, port, hdims, n, e, q):
     from _helpers import oracle_block, run_oracle
     from oracle.sage_ref import random_graph
     from sldm_sage import SageBlock
-    from sldm_sage.dist import DistSageBlock, partition_graph
+    from sldm_sage.dist import DistSageBlock, plan_partition
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -45,7 +46,11 @@ def _worker(rank, world, port, hdims, n, e, q):
         blk = SageBlock(hdims, None, 0.1)
         if rank == 0:
             blk.load_state_dict(ref.state_dict())   # other ranks get it by broadcast
-        part = partition_graph(ei, n, world, rank, backend=CpuBackend)
+        part, info = plan_partition(ei, n, world, rank, hdims[0], 4, strategy=strategy,
+                                    backend=CpuBackend, chunks=chunks)
+        assert info["strategy"] in ("halo", "feature")
+        if strategy != "auto":
+            assert info["strategy"] == strategy
         model = DistSageBlock(blk, part, backend=CpuBackend)
         r0, r1 = part.row_begin, part.row_end
         xl = x[r0:r1].clone().requires_grad_(True)
@@ -65,12 +70,12 @@ def _worker(rank, world, port, hdims, n, e, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 300), (3, 301), (4, 97)])
-def test_dist_sageblock_matches_single_device(world, n):
+def _run(world, n, hdims, strategy, chunks=4):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, [8, 12, 8], n, 6 * n, q))
+    procs = [ctx.Process(target=_worker,
+                         args=(r, world, port, hdims, n, 6 * n, q, strategy, chunks))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -79,3 +84,20 @@ def test_dist_sageblock_matches_single_device(world, n):
         p.join(timeout=60)
     for rank, msg in results:
         assert msg == "ok", f"rank {rank}:\n{msg}"
+
+
+@pytest.mark.parametrize("world,n", [(2, 300), (3, 301), (4, 97)])
+def test_dist_sageblock_matches_single_device(world, n):
+    _run(world, n, [8, 12, 8], "halo")
+
+
+@pytest.mark.parametrize("world,n,chunks", [(2, 300, 4), (3, 301, 3), (4, 97, 1), (4, 10, 8)])
+def test_feature_sliced_sageblock_matches_single_device(world, n, chunks):
+    # F = 8 and 12 over 3-4 ranks: uneven column slices; n = 10 at 4 ranks
+    # with 8 chunks: empty chunks on some ranks
+    _run(world, n, [8, 12, 8], "feature", chunks)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_auto_strategy_matches_single_device(world):
+    _run(world, 200, [16, 16], "auto")
