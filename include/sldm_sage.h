@@ -141,11 +141,16 @@ int sldm_sage_dense_fwd(int dtype, const void* a0, int64_t lda0, int64_t k0,
 /* C[N, nc] = A[N, k] · B[nc, k]^T (both K-contiguous); columns j < scale_cols
  * are divided by max(1, rowptr[i+1]-rowptr[i]) when rowptr != NULL.
  * Backward of lin_l/lin_r w.r.t. their inputs (A8): A = dh, B = [W_l|W_r]^T,
- * giving [dAgg/deg | dx_root] in one pass. */
+ * giving [dAgg/deg | dx_root] in one pass.  With out2 != NULL the columns
+ * j >= scale_cols go to out2[i, j - scale_cols] (ld ldo2) instead, so the
+ * two halves land in separate contiguous [N, F_in] tensors: the transpose
+ * gather then reads dAgg/deg rows from a table half the footprint of the
+ * interleaved buffer (random-row gathers slow down with the table's span,
+ * profiles/r1_gather_probe.txt).  out2 requires scale_cols % 4 == 0. */
 int sldm_gemm_nt_rowscale(int dtype, const void* a, int64_t lda, int64_t k,
                           const void* b, int64_t ldb, int64_t num_rows, int64_t nc,
                           const int32_t* rowptr, int64_t scale_cols,
-                          void* out, int64_t ldo, void* stream);
+                          void* out, int64_t ldo, void* out2, int64_t ldo2, void* stream);
 
 /* out[mo, n0+n1] (fp32) = sum_{r < num_rows} a[r, :]^T ⊗ [b0 | b1][r, :]
  * Weight gradients [dW_l | dW_r] = dh^T · [agg | x] (A8), split over the

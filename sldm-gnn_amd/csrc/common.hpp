@@ -193,7 +193,8 @@ int big_dense_fwd(const void* a0, int64_t lda0, int64_t k0, const void* a1, int6
                   hipStream_t stream);
 int big_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int64_t ldb,
                       int64_t num_rows, int64_t nc, int64_t bn, const int32_t* rowptr,
-                      int64_t scale_cols, void* out, int64_t ldo, hipStream_t stream);
+                      int64_t scale_cols, void* out, int64_t ldo, void* out2, int64_t ldo2,
+                      hipStream_t stream);
 
 // Persistent register-A bf16 kernels (gemm_stream.hip) for K in {256, 512}:
 // the forward at F_out = 256 and the dX GEMM at 256 | 512 output columns.
@@ -211,7 +212,7 @@ int stream_dense_fwd(const void* a0, int64_t lda0, int64_t k0, const void* a1, i
                      hipStream_t stream);
 int stream_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int64_t ldb,
                          int64_t num_rows, int64_t nc, const int32_t* rowptr, int64_t scale_cols,
-                         void* out, int64_t ldo, hipStream_t stream);
+                         void* out, int64_t ldo, void* out2, int64_t ldo2, hipStream_t stream);
 
 }  // namespace sldm
 

@@ -82,8 +82,9 @@ struct NtArgs {
   T* xhat; float* rstd;
   const float* bias; const float* gamma; const float* beta;
   float eps, slope, drop_p, drop_scale; uint64_t seed; int64_t row_off;
-  // EPI_ROWSCALE
+  // EPI_ROWSCALE (out2: optional destination of the columns >= scale_cols)
   const int32_t* rowptr; int scale_cols;
+  T* out2; int64_t ldo2;
 };
 
 template <typename T, bool VEC>
@@ -324,7 +325,7 @@ __global__ __launch_bounds__(kBlock, 2) void gemm_nt_kernel(NtArgs<T> p) {
       for (int j = 0; j < 4; ++j) {
         const int c = min(c0 + j, bn_valid - 1);
         xh[j] = (v[j] - mean) * rstd;
-        const float y = xh[j] * p.gamma[c] + p.beta[c];
+        const float y = __builtin_fmaf(xh[j], p.gamma[c], p.beta[c]);   // as post_bwd recomputes it
         float a = y > 0.f ? y : y * p.slope;
         if (p.drop_p > 0.f) {
           a = sldm::dropout_keep(rkey, (uint32_t)c, sldm::dropout_threshold(p.drop_p))
@@ -352,7 +353,11 @@ __global__ __launch_bounds__(kBlock, 2) void gemm_nt_kernel(NtArgs<T> p) {
         for (int j = 0; j < 4; ++j)
           if (n0 + c0 + j < p.scale_cols) v[j] = v[j] / cnt;
       }
-      T* orow = p.out + row * p.ldo + n0 + c0;
+      // split output: columns >= scale_cols go to out2 (scale_cols % 4 == 0,
+      // so a 4-column group never straddles the split)
+      const bool hi = p.out2 && n0 + c0 >= p.scale_cols;
+      T* orow = hi ? p.out2 + row * p.ldo2 + (n0 + c0 - p.scale_cols)
+                   : p.out + row * p.ldo + n0 + c0;
       if (full4) {
         sldm::Vec<T, 4>::store(orow, v);
       } else {
@@ -685,22 +690,33 @@ extern "C" int sldm_sage_dense_fwd(int dtype, const void* a0, int64_t lda0, int6
 extern "C" int sldm_gemm_nt_rowscale(int dtype, const void* a, int64_t lda, int64_t k,
                                      const void* b, int64_t ldb, int64_t num_rows, int64_t nc,
                                      const int32_t* rowptr, int64_t scale_cols, void* out,
-                                     int64_t ldo, void* stream_) {
+                                     int64_t ldo, void* out2, int64_t ldo2, void* stream_) {
   SLDM_REQUIRE(dtype == SLDM_F32 || dtype == SLDM_BF16, "sldm_gemm_nt_rowscale: dtype %d", dtype);
-  SLDM_REQUIRE(num_rows >= 0 && k > 0 && nc > 0 && ldo >= nc && lda >= k && ldb >= k,
+  SLDM_REQUIRE(num_rows >= 0 && k > 0 && nc > 0 && lda >= k && ldb >= k,
                "sldm_gemm_nt_rowscale: bad sizes");
+  if (out2) {
+    SLDM_REQUIRE(scale_cols > 0 && scale_cols < nc && scale_cols % 4 == 0 &&
+                     ldo >= scale_cols && ldo2 >= nc - scale_cols,
+                 "sldm_gemm_nt_rowscale: split output needs 0 < scale_cols < nc, "
+                 "scale_cols %% 4 == 0 and ld >= the half widths");
+  } else {
+    SLDM_REQUIRE(ldo >= nc, "sldm_gemm_nt_rowscale: ldo < nc");
+  }
   if (num_rows == 0) return SLDM_OK;
   SLDM_REQUIRE(a && b && out, "sldm_gemm_nt_rowscale: NULL argument");
   hipStream_t stream = sldm::as_stream(stream_);
   if (dtype == SLDM_BF16 && sldm::stream_gemm_enabled() &&
-      sldm::stream_rowscale_ok(k, nc, a, lda, b, ldb, out, ldo, scale_cols))
+      sldm::stream_rowscale_ok(k, nc, a, lda, b, ldb, out, ldo, scale_cols) &&
+      (!out2 || (ldo2 == ldo && scale_cols % 256 == 0 &&
+                 sldm::stream_rowscale_ok(k, nc, a, lda, b, ldb, out2, ldo2, scale_cols))))
     return sldm::stream_gemm_rowscale(a, lda, k, b, ldb, num_rows, nc, rowptr, scale_cols, out,
-                                      ldo, stream);
+                                      ldo, out2, ldo2, stream);
   if (dtype == SLDM_BF16 && sldm::big_gemm_enabled() && nc % 128 == 0) {
     const int64_t bn = nc % 256 == 0 ? 256 : 128;
-    if (sldm::big_gemm_ok(k, k, bn, a, lda, a, lda, b, ldb, ldo))
+    if (sldm::big_gemm_ok(k, k, bn, a, lda, a, lda, b, ldb, out2 ? 4 : ldo) &&
+        (!out2 || (ldo % 4 == 0 && ldo2 % 4 == 0)))
       return sldm::big_gemm_rowscale(a, lda, k, b, ldb, num_rows, nc, bn, rowptr, scale_cols,
-                                     out, ldo, stream);
+                                     out, ldo, out2, ldo2, stream);
   }
   auto fill = [&](auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
@@ -711,6 +727,7 @@ extern "C" int sldm_gemm_nt_rowscale(int dtype, const void* a, int64_t lda, int6
     p.b = (const T*)b; p.ldb = ldb;
     p.M = num_rows; p.Nc = (int)nc;
     p.out = (T*)out; p.ldo = ldo;
+    p.out2 = (T*)out2; p.ldo2 = ldo2;
     p.rowptr = rowptr; p.scale_cols = (int)scale_cols;
     return launch_nt<T, EPI_ROWSCALE>(p, stream);
   };

@@ -49,6 +49,7 @@ struct BigArgs {
   const float* bias; const float* gamma; const float* beta;
   float eps, slope, drop_p, drop_scale; uint64_t seed; int64_t row_off;
   const int32_t* rowptr; int scale_cols;
+  uint16_t* out2; int64_t ldo2;               // optional home of columns >= scale_cols
 };
 
 __device__ __forceinline__ void dma16(const void* g, char* lds_base) {
@@ -251,7 +252,11 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_big_kernel(BigArgs p) {
           v[r] = acc[m][t][r];
           if (c + r < p.scale_cols) v[r] = v[r] / cnt;
         }
-        if (c < p.Nc) sldm::Vec<uint16_t, 4>::store(p.out + row * p.ldo + c, v);
+        if (c < p.Nc) {
+          uint16_t* dst = p.out2 && c >= p.scale_cols ? p.out2 + row * p.ldo2 + (c - p.scale_cols)
+                                                      : p.out + row * p.ldo + c;
+          sldm::Vec<uint16_t, 4>::store(dst, v);
+        }
       }
     }
   }
@@ -317,7 +322,8 @@ int big_dense_fwd(const void* a0, int64_t lda0, int64_t k0, const void* a1, int6
 
 int big_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int64_t ldb,
                       int64_t num_rows, int64_t nc, int64_t bn, const int32_t* rowptr,
-                      int64_t scale_cols, void* out, int64_t ldo, hipStream_t stream) {
+                      int64_t scale_cols, void* out, int64_t ldo, void* out2, int64_t ldo2,
+                      hipStream_t stream) {
   BigArgs p{};
   p.a0 = (const uint16_t*)a; p.lda0 = lda; p.k0 = (int)k;
   p.a1 = (const uint16_t*)a; p.lda1 = lda;
@@ -326,6 +332,7 @@ int big_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int6
   p.M = num_rows; p.Nc = (int)nc; p.bn = (int)bn;
   p.grid_y = (int)((nc + bn - 1) / bn);
   p.out = (uint16_t*)out; p.ldo = ldo;
+  p.out2 = (uint16_t*)out2; p.ldo2 = ldo2;
   p.rowptr = rowptr; p.scale_cols = (int)scale_cols;
   return bn == 256 ? launch_big<8, BIG_ROWSCALE>(p, stream)
                    : launch_big<4, BIG_ROWSCALE>(p, stream);

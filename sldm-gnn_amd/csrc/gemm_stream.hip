@@ -55,6 +55,7 @@ struct StreamArgs {
   const float* bias; const float* gamma; const float* beta;
   float eps, slope, drop_p, drop_scale; uint64_t seed; int64_t row_off;
   const int32_t* rowptr; int scale_cols;
+  uint16_t* out2; int64_t ldo2;               // ROWSCALE: optional home of columns >= scale_cols
 };
 
 __device__ __forceinline__ int swz(int r16) { return (r16 >> 2) & 2; }
@@ -355,6 +356,11 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
         }
       }
     } else {
+      // Split output (host-checked: scale_cols a multiple of 256, ldo2 == ldo):
+      // a wave's 256 columns all go to one buffer, so only its uniform base
+      // moves and no second per-lane row offset is live.
+      uint16_t* obase = p.out;
+      if (p.out2 && wc * 256 >= p.scale_cols) obase = p.out2 - p.scale_cols;
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
         // clamped like the loads: rows past M rewrite row M-1's own values
@@ -371,7 +377,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = scaled ? acc[m][t][r] * inv : acc[m][t][r];
-          sldm::Vec<uint16_t, 4>::store(p.out + row * p.ldo + c, v);
+          sldm::Vec<uint16_t, 4>::store(obase + row * p.ldo + c, v);
         }
       }
     }
@@ -476,13 +482,14 @@ int stream_dense_fwd(const void* a0, int64_t lda0, int64_t k0, const void* a1, i
 
 int stream_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int64_t ldb,
                          int64_t num_rows, int64_t nc, const int32_t* rowptr, int64_t scale_cols,
-                         void* out, int64_t ldo, hipStream_t stream) {
+                         void* out, int64_t ldo, void* out2, int64_t ldo2, hipStream_t stream) {
   StreamArgs p{};
   p.a0 = (const uint16_t*)a; p.lda0 = lda; p.k0 = (int)k;
   p.a1 = (const uint16_t*)a; p.lda1 = lda;
   p.b = (const uint16_t*)b; p.ldb = ldb;
   p.M = num_rows; p.Nc = (int)nc;
   p.out = (uint16_t*)out; p.ldo = ldo;
+  p.out2 = (uint16_t*)out2; p.ldo2 = ldo2;
   p.rowptr = rowptr; p.scale_cols = (int)scale_cols;
   auto go = [&](auto hasdeg) -> int {
     constexpr bool HD = decltype(hasdeg)::value;

@@ -73,7 +73,7 @@ __global__ __launch_bounds__(kBlock) void post_fwd_kernel(
     for (int k = 0; k < V; ++k) {
       const int f = f0[c] + k;
       xh[k] = (v[c][k] - mean) * rstd;
-      float y = xh[k] * gamma[f] + beta[f];
+      float y = __builtin_fmaf(xh[k], gamma[f], beta[f]);   // the backward recomputes this
       float a = y > 0.0f ? y : y * slope;
       z[k] = keep[k] ? a * drop_scale : 0.0f;
     }
@@ -107,66 +107,89 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
     f0[c] = act[c] ? f : feat - V;
   }
   float pg[NCH][V], pb[NCH][V], pd[NCH][V];
+  // gamma / beta of this thread's (fixed) columns, once
+  float gm[NCH][V], bt[NCH][V];
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
-    for (int k = 0; k < V; ++k) pg[c][k] = pb[c][k] = pd[c][k] = 0.0f;
+    for (int k = 0; k < V; ++k) {
+      pg[c][k] = pb[c][k] = pd[c][k] = 0.0f;
+      gm[c][k] = gamma[f0[c] + k];
+      bt[c][k] = beta[f0[c] + k];
+    }
 
   const float inv_f = 1.0f / (float)feat;
+  const uint32_t dthr = sldm::dropout_threshold(drop_p);
+  // RB rows per thread group and iteration, all loads issued before the
+  // first use (bytes in flight: this kernel is HBM-bound)
+  constexpr int RB = 2;
   const int64_t stride = (int64_t)gridDim.x * groups_per_block;
-  const int64_t nrounds = (nrows + stride - 1) / stride;
+  const int64_t nrounds = (nrows + RB * stride - 1) / (RB * stride);
   for (int64_t it = 0; it < nrounds; ++it) {
-    const int64_t row = it * stride + (int64_t)blockIdx.x * groups_per_block + group;
-    const bool live = row < nrows;
-    const int64_t r = live ? row : 0;
-    const float rs = rstd[r];
-    const uint32_t rkey = sldm::dropout_row_key(seed, (uint64_t)(r + row_off));
-    const uint32_t dthr = sldm::dropout_threshold(drop_p);
-    float xh[NCH][V], gx[NCH][V], dy[NCH][V];
-    float s1 = 0.0f, s2 = 0.0f;
+    int64_t rr[RB];
+    bool live[RB];
+    float go[RB][NCH][V], xh[RB][NCH][V], zo[RB][NCH][V];
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      float go[V], zo[V];
-      sldm::Vec<T, V>::load(dout + r * (int64_t)feat + f0[c], go);
-      sldm::Vec<T, V>::load(xhat + r * (int64_t)feat + f0[c], xh[c]);
-      if (zout) sldm::Vec<T, V>::load(zout + r * (int64_t)feat + f0[c], zo);
-      bool kp[V];
+    for (int u = 0; u < RB; ++u) {
+      const int64_t row = (it * RB + u) * stride + (int64_t)blockIdx.x * groups_per_block + group;
+      live[u] = row < nrows;
+      rr[u] = live[u] ? row : 0;
 #pragma unroll
-      for (int k = 0; k < V; ++k) kp[k] = true;
-      if (drop_p > 0.0f) sldm::dropout_keepv<V>(rkey, (uint32_t)f0[c], dthr, kp);
-#pragma unroll
-      for (int k = 0; k < V; ++k) {
-        const int f = f0[c] + k;
-        const float g = gamma[f];
-        const bool keep = kp[k];
-        float d = keep ? go[k] * drop_scale : 0.0f;
-        // Activation branch: from the saved output when given (sign(z) ==
-        // sign(y) exactly, even with bf16 storage); else from y = xhat*g+b,
-        // which a rounded xhat can flip where |y| is tiny.
-        const bool pos = zout ? (keep ? zo[k] > 0.0f : true) : (xh[c][k] * g + beta[f] > 0.0f);
-        d = pos ? d : d * slope;
-        if (!act[c] || !live) { d = 0.0f; xh[c][k] = 0.0f; }
-        dy[c][k] = d;
-        gx[c][k] = d * g;
-        s1 += gx[c][k];
-        s2 += gx[c][k] * xh[c][k];
+      for (int c = 0; c < NCH; ++c) {
+        sldm::Vec<T, V>::load(dout + rr[u] * (int64_t)feat + f0[c], go[u][c]);
+        sldm::Vec<T, V>::load(xhat + rr[u] * (int64_t)feat + f0[c], xh[u][c]);
+        if (zout) sldm::Vec<T, V>::load(zout + rr[u] * (int64_t)feat + f0[c], zo[u][c]);
       }
     }
-    const float m1 = group_sum(s1, lpr) * inv_f;
-    const float m2 = group_sum(s2, lpr) * inv_f;
-    if (!live) continue;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      if (!act[c]) continue;
-      float o[V];
+    for (int u = 0; u < RB; ++u) {
+      const int64_t r = rr[u];
+      const float rs = rstd[r];
+      const uint32_t rkey = sldm::dropout_row_key(seed, (uint64_t)(r + row_off));
+      float gx[NCH][V], dy[NCH][V];
+      float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll
-      for (int k = 0; k < V; ++k) {
-        o[k] = rs * (gx[c][k] - m1 - xh[c][k] * m2);
-        pg[c][k] += dy[c][k] * xh[c][k];
-        pb[c][k] += dy[c][k];
-        pd[c][k] += o[k];
+      for (int c = 0; c < NCH; ++c) {
+        bool kp[V];
+#pragma unroll
+        for (int k = 0; k < V; ++k) kp[k] = true;
+        if (drop_p > 0.0f) sldm::dropout_keepv<V>(rkey, (uint32_t)f0[c], dthr, kp);
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+          const float g = gm[c][k];
+          const bool keep = kp[k];
+          float d = keep ? go[u][c][k] * drop_scale : 0.0f;
+          // Activation branch: from the saved output when given (sign(z) ==
+          // sign(y) exactly, even with bf16 storage); else from
+          // y = fma(xhat, g, b), the forward epilogues' exact expression
+          // (bit-equal y for fp32 storage; a bf16-rounded xhat can flip only
+          // |y| within half an ulp of 0).
+          const bool pos = zout ? (keep ? zo[u][c][k] > 0.0f : true)
+                                : (__builtin_fmaf(xh[u][c][k], g, bt[c][k]) > 0.0f);
+          d = pos ? d : d * slope;
+          if (!act[c] || !live[u]) { d = 0.0f; xh[u][c][k] = 0.0f; }
+          dy[c][k] = d;
+          gx[c][k] = d * g;
+          s1 += gx[c][k];
+          s2 += gx[c][k] * xh[u][c][k];
+        }
       }
-      sldm::Vec<TD, V>::store(dh + r * (int64_t)feat + f0[c], o);
+      const float m1 = group_sum(s1, lpr) * inv_f;
+      const float m2 = group_sum(s2, lpr) * inv_f;
+      if (!live[u]) continue;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        if (!act[c]) continue;
+        float o[V];
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+          o[k] = rs * (gx[c][k] - m1 - xh[u][c][k] * m2);
+          pg[c][k] += dy[c][k] * xh[u][c][k];
+          pb[c][k] += dy[c][k];
+          pd[c][k] += o[k];
+        }
+        sldm::Vec<TD, V>::store(dh + r * (int64_t)feat + f0[c], o);
+      }
     }
   }
 

@@ -49,7 +49,8 @@ _SIGNATURES = {
                                            ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                            ctypes.c_uint64, _c_i64, _vp, _vp, _vp, _vp]),
     "sldm_gemm_nt_rowscale": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _c_i64, _vp, _c_i64,
-                                             _c_i64, _c_i64, _vp, _c_i64, _vp, _c_i64, _vp]),
+                                             _c_i64, _c_i64, _vp, _c_i64, _vp, _c_i64, _vp,
+                                             _c_i64, _vp]),
     "sldm_gemm_tn_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, _c_i64]),
     "sldm_gemm_tn": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64,
                                     _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, ctypes.c_size_t,

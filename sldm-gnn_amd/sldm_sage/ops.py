@@ -193,19 +193,31 @@ def sage_dense_fwd(agg: torch.Tensor, x: torch.Tensor, wcat: torch.Tensor, bias,
 
 
 def gemm_nt_rowscale(a: torch.Tensor, b: torch.Tensor, rowptr: torch.Tensor | None,
-                     scale_cols: int) -> torch.Tensor:
-    """C = a · b^T, columns < scale_cols divided by max(1, deg(row))."""
+                     scale_cols: int, split: bool = False):
+    """C = a · b^T, columns < scale_cols divided by max(1, deg(row)).
+
+    ``split``: return (C[:, :scale_cols], C[:, scale_cols:]) as two separate
+    contiguous tensors (one launch) instead of one [n, nc] tensor."""
     dev = _require_gpu(a, b, rowptr)
     assert a.stride(1) == 1 and b.is_contiguous() and a.dtype == b.dtype
     n, k = a.shape
     nc = b.size(0)
-    out = torch.empty(n, nc, dtype=a.dtype, device=dev)
+    if split:
+        if not 0 < scale_cols < nc or scale_cols % 4:
+            raise ValueError("gemm_nt_rowscale(split=True) needs 0 < scale_cols < nc, "
+                             "scale_cols % 4 == 0")
+        out = torch.empty(n, scale_cols, dtype=a.dtype, device=dev)
+        out2 = torch.empty(n, nc - scale_cols, dtype=a.dtype, device=dev)
+    else:
+        out = torch.empty(n, nc, dtype=a.dtype, device=dev)
+        out2 = None
     with _Timed("dense_bwd_data", (n * k + n * nc) * a.element_size()):
         _lib.check(_lib.load().sldm_gemm_nt_rowscale(
             dtype_code(a), a.data_ptr(), a.stride(0), k, b.data_ptr(), b.stride(0), n, nc,
-            _ptr(rowptr), scale_cols, out.data_ptr(), out.stride(0), _stream(dev)),
+            _ptr(rowptr), scale_cols, out.data_ptr(), out.stride(0), _ptr(out2),
+            out2.stride(0) if out2 is not None else 0, _stream(dev)),
             "sldm_gemm_nt_rowscale")
-    return out
+    return (out, out2) if split else out
 
 
 def gemm_tn(a: torch.Tensor, b0: torch.Tensor, b1: torch.Tensor | None) -> torch.Tensor:
@@ -249,6 +261,21 @@ def post_fwd(h: torch.Tensor, bias, gamma, beta, eps: float, slope: float, drop_
     return out, xhat, rstd
 
 
+def branch_source(out: torch.Tensor) -> torch.Tensor | None:
+    """What the post backward reads to pick the activation branch.
+
+    Default None: sign(y) is recomputed from the saved xhat as
+    y = fma(xhat, gamma, beta) -- bit-identical to the forward's y for fp32
+    storage; with bf16 storage only |y| within half an xhat ulp of 0 can flip
+    (the elements whose sign bf16 already leaves undetermined against an fp32
+    reference).  SLDM_ACT_BRANCH_FROM_OUTPUT=1 reads the saved layer output
+    instead (exact sign in bf16 too, one more [N, F] read per layer)."""
+    return out if _BRANCH_FROM_OUTPUT else None
+
+
+_BRANCH_FROM_OUTPUT = __import__("os").environ.get("SLDM_ACT_BRANCH_FROM_OUTPUT") == "1"
+
+
 def post_bwd(dout: torch.Tensor, xhat: torch.Tensor, rstd: torch.Tensor, gamma, beta,
              slope: float, drop_p: float, seed: int, dh_dtype: torch.dtype,
              zout: torch.Tensor | None = None, row_offset: int = 0):
@@ -268,7 +295,8 @@ def post_bwd(dout: torch.Tensor, xhat: torch.Tensor, rstd: torch.Tensor, gamma, 
     cols = torch.empty(3 * F, dtype=torch.float32, device=dev)
     gamma_ = gamma.detach().float().contiguous()
     beta_ = beta.detach().float().contiguous()
-    with _Timed("post_bwd", N * F * (2 * xhat.element_size() + dh.element_size())):
+    with _Timed("post_bwd", N * F * ((3 if zout is not None else 2) * xhat.element_size()
+                                     + dh.element_size())):
         _lib.check(lib.sldm_post_bwd(
             dtype_code(xhat), dout.data_ptr(), xhat.data_ptr(), _ptr(zout), rstd.data_ptr(), N, F,
             gamma_.data_ptr(), beta_.data_ptr(), float(slope), float(drop_p),

@@ -65,8 +65,9 @@ class _SageLayerFn(torch.autograd.Function):
         out, xhat, rstd = dense.sage_layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope,
                                                drop_p, seed, save=needs_grad)
         if needs_grad:
-            # `out` is saved too (it is the next layer's input anyway): its sign
-            # fixes the activation branch exactly in the backward.
+            # `out` is saved too (it is the next layer's input anyway): with
+            # SLDM_ACT_BRANCH_FROM_OUTPUT=1 its sign picks the activation
+            # branch in the backward (ops.branch_source).
             ctx.save_for_backward(x, agg, xhat, rstd, wl, wr, gamma, beta, out)
             ctx.graph = graph
             ctx.cfg = (slope, drop_p, seed)
@@ -78,7 +79,7 @@ class _SageLayerFn(torch.autograd.Function):
         graph: SageGraph = ctx.graph
         slope, drop_p, seed = ctx.cfg
         dh, dgamma, dbeta, dbl = ops.post_bwd(dout, xhat, rstd, gamma, beta, slope, drop_p, seed,
-                                              dh_dtype=x.dtype, zout=out)
+                                              dh_dtype=x.dtype, zout=ops.branch_source(out))
         dwl, dwr = dense.sage_linear_bwd_weight(dh, agg, x)
         dx = None
         if ctx.needs_input_grad[0]:

@@ -501,6 +501,11 @@ def test_gemm_nt_rowscale_and_tn_vs_torch(m, fi, fo, dtype):
     ref[:, :fi] /= deg[:, None]
     tol = dict(atol=1e-4, rtol=1e-4) if dtype == torch.float32 else dict(atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(out.float().cpu(), ref, **tol)
+    if fi % 4 == 0:
+        # split output: the same bits in two contiguous tensors
+        lo, hi = ops.gemm_nt_rowscale(dh.to(DEV), wt.to(DEV), g.rowptr, fi, split=True)
+        assert lo.is_contiguous() and hi.is_contiguous()
+        assert torch.equal(lo, out[:, :fi]) and torch.equal(hi, out[:, fi:])
     # weight grads: dh^T [agg | x]
     agg, x = (torch.randn(m, fi, generator=gen).to(dtype) for _ in range(2))
     dw = ops.gemm_tn(dh.to(DEV), agg.to(DEV), x.to(DEV))
@@ -580,6 +585,12 @@ def test_stream_gemm_rowscale_vs_torch(m, fi):
     deg = (g.rowptr[1:] - g.rowptr[:-1]).clamp(min=1).float()
     ref[:, :fi] /= deg[:, None]
     torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=2e-2)
+    # split output (fi = 256: the same stream kernel, same bits; fi = 128: the
+    # split falls back to the big-tile kernel, equal within bf16 rounding)
+    lo, hi = ops.gemm_nt_rowscale(dh, wt, g.rowptr, fi, split=True)
+    if fi % 256 == 0:
+        assert torch.equal(lo, out[:, :fi]) and torch.equal(hi, out[:, fi:])
+    torch.testing.assert_close(torch.cat([lo, hi], 1).float(), ref, atol=3e-2, rtol=2e-2)
 
 
 # ------------------------------------------------ overlapped (split) gather --

@@ -82,6 +82,9 @@ def main():
     if want("nt"):
         add("gemm_nt_rowscale N=2f", timeit(lambda: ops.gemm_nt_rowscale(dh, wt, gr.rowptr, f),
                                             a.reps), (n * f + n * 2 * f) * s, fl)
+        add("gemm_nt_rowscale N=2f split", timeit(
+            lambda: ops.gemm_nt_rowscale(dh, wt, gr.rowptr, f, split=True), a.reps),
+            (n * f + n * 2 * f) * s, fl)
         add("gemm_nt_rowscale N=f", timeit(lambda: ops.gemm_nt_rowscale(dh, wcat[:, :f].contiguous(),
                                                                          None, 0), a.reps),
             (n * f + n * f) * s, fl / 2)
@@ -89,8 +92,10 @@ def main():
         add("gemm_tn", timeit(lambda: ops.gemm_tn(dh, agg, x), a.reps), 3 * n * f * s, fl)
     if want("post"):
         out, xh, rs = ops.post_fwd(dh, None, gam, bet, 1e-5, 0.1, 0.0, 0, dt, True)
-        add("post_bwd", timeit(lambda: ops.post_bwd(dh, xh, rs, gam, bet, 0.1, 0.0, 0, dt),
-                               a.reps), 3 * n * f * s)
+        for p_, zo in [(0.0, None), (0.25, None), (0.25, out)]:
+            add(f"post_bwd p={p_} zout={zo is not None}",
+                timeit(lambda: ops.post_bwd(dh, xh, rs, gam, bet, 0.1, p_, 3, dt, zout=zo),
+                       a.reps), (3 + (zo is not None)) * n * f * s)
     if want("torch"):
         add("torch.mm [agg|x]W^T", timeit(lambda: torch.mm(torch.cat([agg, x], 1), wcat.t()),
                                            a.reps), 3 * n * f * s, fl)
