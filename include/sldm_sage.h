@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SLDM_ABI_VERSION 1
+#define SLDM_ABI_VERSION 2
 
 enum sldm_dtype { SLDM_F32 = 0, SLDM_BF16 = 1 };
 enum sldm_status { SLDM_OK = 0, SLDM_ERR_ARG = 1, SLDM_ERR_HIP = 2 };
@@ -162,6 +162,42 @@ int sldm_gemm_tn(int dtype, const void* a, int64_t lda, int64_t mo,
                  const void* b1, int64_t ldb1, int64_t n1,
                  int64_t num_rows, float* out, void* workspace, size_t workspace_bytes,
                  void* stream);
+
+/* ------------------------------------------------- graph-level readout ---
+ * Global mean / max pooling over the batch vector:
+ * replaces PyG 2.7.0 global_mean_pool / global_max_pool (grusage.py:3,
+ * :119-127, :185), i.e. utils.scatter(x, batch, reduce='mean' | 'max') --
+ * zeros(B,F).scatter_reduce_(0, batch, x, 'amax', include_self=False) on the
+ * reference's CPU path.  The batch arrives as a segment CSR: seg_rowptr
+ * [B+1] and member [N] (node ids, ascending within a segment; sldm_csr_build
+ * of [arange(N); batch]).  Segments are processed in pieces of
+ * sldm_segment_pool_piece_rows() rows: piece_ptr [B+1] is the prefix sum of
+ * ceil(len_s / piece_rows) (num_pieces = piece_ptr[B]).
+ * mean_out / max_out: [B, F] (either may be NULL); empty segments give 0.
+ * max_divisor (fp32 [B, F], may be NULL): the number the upstream max
+ * gradient is divided by -- members equal to the max, plus 1 when the max is
+ * 0 (torch's amax backward also counts the zero-initialised self there).
+ * max_first_row (int32 [B, F], may be NULL): the first member row holding
+ * the max (x.max(dim) routing, PyG's batch=None global_max_pool). */
+int sldm_segment_pool_piece_rows(void);
+size_t sldm_segment_pool_workspace_bytes(int64_t num_pieces, int64_t feat);
+int sldm_segment_pool(int dtype, const void* x, int64_t ldx, const int32_t* seg_rowptr,
+                      const int32_t* member, int64_t num_segments, const int32_t* piece_ptr,
+                      int64_t num_pieces, int64_t feat, void* mean_out, int64_t ld_mean,
+                      void* max_out, int64_t ld_max, float* max_divisor,
+                      int32_t* max_first_row, void* workspace, size_t workspace_bytes,
+                      void* stream);
+
+/* dx[i] = dmean[b]/count_b + (x[i] == max[b] ? dmax[b] / max_divisor[b] : 0),
+ * b = seg_of[i] (int64, the batch vector); with max_first_row != NULL the max
+ * term is instead dmax[b] at i == max_first_row[b] (x, max_out, max_divisor
+ * unused).  dmean or dmax may be NULL. */
+int sldm_segment_pool_bwd(int dtype, const void* x, int64_t ldx, const int64_t* seg_of,
+                          const int32_t* seg_rowptr, int64_t num_nodes, int64_t feat,
+                          const void* dmean, int64_t ld_dmean, const void* max_out,
+                          int64_t ld_max, const void* dmax, int64_t ld_dmax,
+                          const float* max_divisor, const int32_t* max_first_row, void* dx,
+                          int64_t ld_dx, void* stream);
 
 #ifdef __cplusplus
 }
