@@ -199,6 +199,26 @@ int sldm_segment_pool_bwd(int dtype, const void* x, int64_t ldx, const int64_t* 
                           const float* max_divisor, const int32_t* max_first_row, void* dx,
                           int64_t ld_dx, void* stream);
 
+/* ------------------------------------------------ graph construction ---
+ * Radius edges of a vehicle pack, replacing the
+ * O(V^2 T) pair loop of gbuilder.py:85-111 / :241-268: for i, for j != i,
+ * d = per-frame XY distance over the frames both vehicles are present in
+ * (presence > 0.5); if any and min(d) <= radius: edge (i, j) with attr
+ * [min, max, mean, mean of squares] -- numpy float32 arithmetic and order
+ * reproduced exactly, edges i-major / j ascending.
+ * pos: element strides (vehicle, frame, coordinate) of X (Y = X + sc);
+ * presence: strides (vehicle, frame).  num_frames <= 256.
+ * edge_index: int64 [2, capacity] (row 1 at + capacity), edge_attr fp32
+ * [capacity, 4], capacity >= V(V-1); num_edges: device int32 (the edges
+ * written, first num_edges columns). */
+size_t sldm_radius_edges_workspace_bytes(int64_t num_vehicles);
+int sldm_radius_edges(const float* pos, int64_t pos_sv, int64_t pos_st, int64_t pos_sc,
+                      const float* presence, int64_t pres_sv, int64_t pres_st,
+                      int64_t num_vehicles, int64_t num_frames, float radius,
+                      int64_t* edge_index, int64_t capacity, float* edge_attr,
+                      int32_t* num_edges, void* workspace, size_t workspace_bytes,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -63,6 +63,10 @@ _SIGNATURES = {
     "sldm_segment_pool_bwd": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _vp, _vp, _c_i64, _c_i64,
                                              _vp, _c_i64, _vp, _c_i64, _vp, _c_i64, _vp, _vp,
                                              _vp, _c_i64, _vp]),
+    "sldm_radius_edges_workspace_bytes": (ctypes.c_size_t, [_c_i64]),
+    "sldm_radius_edges": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _c_i64,
+                                         _c_i64, _c_i64, ctypes.c_float, _vp, _c_i64, _vp, _vp,
+                                         _vp, ctypes.c_size_t, _vp]),
 }
 
 _lock = threading.Lock()

@@ -110,6 +110,21 @@ class _GraphCache:
             self._entries[key] = (ref, ver, num_nodes, graph)
         return graph
 
+    def put(self, edge_index: torch.Tensor, num_nodes: int, graph: SageGraph) -> None:
+        """Register a CSR built elsewhere (e.g. at collate time) for this
+        edge_index tensor, so the next SageBlock call skips the GPU build."""
+        if edge_index.is_inference() or graph.device != edge_index.device:
+            return
+        key = id(edge_index)
+        try:
+            ref = weakref.ref(edge_index, lambda _r, k=key: self._drop(k))
+        except TypeError:
+            return
+        with self._lock:
+            if len(self._entries) >= self._max and key not in self._entries:
+                self._entries.pop(next(iter(self._entries)))
+            self._entries[key] = (ref, edge_index._version, num_nodes, graph)
+
     def clear(self) -> None:
         with self._lock:
             self._entries.clear()
