@@ -17,11 +17,15 @@ def weight_cat(wl: torch.Tensor, wr: torch.Tensor, dtype: torch.dtype) -> torch.
 
 
 def sage_layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p, seed, save,
-                   row_offset=0):
-    """out = dropout(act(LN(agg·W_l^T + b_l + x·W_r^T)))  -> (out, xhat, rstd)."""
-    wcat = weight_cat(wl, wr, x.dtype)
+                   row_offset=0, outs=None, wcat=None):
+    """out = dropout(act(LN(agg·W_l^T + b_l + x·W_r^T)))  -> (out, xhat, rstd).
+
+    ``outs``: preallocated (out, xhat, rstd) row slices; ``wcat``: the
+    [W_l | W_r] operand when the caller already built it."""
+    if wcat is None:
+        wcat = weight_cat(wl, wr, x.dtype)
     return ops.sage_dense_fwd(agg, x, wcat, bl, gamma, beta, eps, slope, drop_p, seed, save,
-                              row_offset)
+                              row_offset, outs=outs)
 
 
 def sage_linear_bwd_data(dh: torch.Tensor, wl: torch.Tensor, wr: torch.Tensor,

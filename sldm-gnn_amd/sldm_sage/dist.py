@@ -95,10 +95,12 @@ class HipBackend:
         return ops.gather_rows(x, rowptr, idx, idx.numel(), mean=False, name="halo_pack")
 
     @staticmethod
-    def layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p, seed, save, row_offset):
+    def layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p, seed, save, row_offset,
+                  outs=None):
+        """Fused dense + post stack; ``outs`` = preallocated (out, xhat, rstd)."""
         from . import dense
         return dense.sage_layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p, seed,
-                                    save, row_offset=row_offset)
+                                    save, row_offset=row_offset, outs=outs)
 
     @staticmethod
     def post_bwd(dout, xhat, rstd, gamma, beta, slope, drop_p, seed, zout, row_offset):
@@ -507,19 +509,55 @@ def _wait_all(works):
 
 
 class _FeatLayerFn(torch.autograd.Function):
+    """One feature-sliced layer, pipelined per row chunk j:
+    gather(j) || col->row(j-1) on the RCCL stream; then, as each chunk's
+    aggregate arrives, dense + LayerNorm on its rows and (when a next layer
+    follows) row->col(j) of its output, which runs while later chunks compute
+    -- the next layer's column-sliced input is already in flight when this
+    layer returns (handed over in ``carry``)."""
+
     @staticmethod
     def forward(ctx, x, wl, bl, wr, gamma, beta, part: FeaturePartition, group, backend,
-                slope, drop_p, seed, eps):
+                slope, drop_p, seed, eps, carry: dict):
         g = part.graph
         F = x.size(1)
-        x_cols, works = _feat_rows_to_cols(part, x, group)
+        fo = wl.size(0)
+        pre = carry.pop("cols", None)
+        x_cols, works = pre if pre is not None else _feat_rows_to_cols(part, x, group)
         _wait_all(works)
-        agg = _feat_aggregate_to_rows(backend, part, x_cols, g.rowptr, g.col, True, F,
-                                      part.chunk_edges, group)
-        del x_cols
+        out_cols = x_cols.new_empty(part.num_nodes, x_cols.size(1))
+        pending = []
+        for j in range(part.num_chunks):
+            _feat_gather(backend, x_cols, g.rowptr, g.col, part, j, True, out_cols,
+                         part.chunk_edges[j])
+            pending.append(_cols_to_rows(part, out_cols, j, F, group))
         save = any(ctx.needs_input_grad[:6])
-        out, xhat, rstd = backend.layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p,
-                                            seed, save, part.row_begin)
+        n = part.num_rows
+        agg = x.new_empty(n, F)
+        out = x.new_empty(n, fo)
+        xhat = x.new_empty(n, fo) if save else None
+        rstd = x.new_empty(n, dtype=torch.float32) if save else None
+        nxt = None
+        if carry.get("next_layer"):
+            cs = part.col_sizes(fo)
+            nxt = (x.new_empty(part.num_nodes, cs[part.rank]), [])
+        for j, (work, recv, cs_in) in enumerate(pending):
+            a, b = part.own_chunk[j], part.own_chunk[j + 1]
+            if work is not None:
+                work.wait()
+            _cols_to_rows_finish(part, recv, cs_in, b - a, agg[a:b])
+            if b > a:
+                backend.layer_fwd(agg[a:b], x[a:b], wl, bl, wr, gamma, beta, eps, slope, drop_p,
+                                  seed, save, part.row_begin + a,
+                                  outs=(out[a:b], xhat[a:b] if save else None,
+                                        rstd[a:b] if save else None))
+            if nxt is not None:
+                w, keep = _rows_to_cols(part, out, j, nxt[0], group)
+                if w is not None:
+                    nxt[1].append((w, keep))
+        del x_cols, out_cols, pending
+        if nxt is not None:
+            carry["cols"] = nxt
         if save:
             ctx.save_for_backward(x, agg, xhat, rstd, wl, wr, gamma, beta, out)
             ctx.part, ctx.group, ctx.backend = part, group, backend
@@ -553,7 +591,7 @@ class _FeatLayerFn(torch.autograd.Function):
         dwl, dbl, dwr, dgamma, dbeta = (c.view_as(t) for c, t in zip(
             torch.split(flat, [t.numel() for t in grads]), grads))
         return (dx, dwl.to(wl.dtype), dbl.to(wl.dtype), dwr.to(wr.dtype), dgamma.to(gamma.dtype),
-                dbeta.to(beta.dtype), None, None, None, None, None, None, None)
+                dbeta.to(beta.dtype), None, None, None, None, None, None, None, None)
 
 
 class _DistLayerFn(torch.autograd.Function):
@@ -631,15 +669,21 @@ class DistSageBlock(nn.Module):
 
     def forward(self, x_local: torch.Tensor) -> torch.Tensor:
         from .sageblock import _act_slope, _drop_p, _new_seed
-        fn = _FeatLayerFn if isinstance(self.part, FeaturePartition) else _DistLayerFn
+        feat = isinstance(self.part, FeaturePartition)
         x = x_local.contiguous()
-        for conv, post in zip(self.block.convs, self.block.posts):
+        layers = list(zip(self.block.convs, self.block.posts))
+        carry: dict = {}
+        for i, (conv, post) in enumerate(layers):
             ln, act, drop = post[0], post[1], post[2]
             p = _drop_p(drop)
             seed = _new_seed() if p > 0 else 0
-            x = fn.apply(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight,
-                                   ln.weight, ln.bias, self.part, self.group, self.backend,
-                                   _act_slope(act), p, seed, float(ln.eps))
+            args = (x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, ln.weight, ln.bias,
+                    self.part, self.group, self.backend, _act_slope(act), p, seed, float(ln.eps))
+            if feat:
+                carry["next_layer"] = i + 1 < len(layers)
+                x = _FeatLayerFn.apply(*args, carry)
+            else:
+                x = _DistLayerFn.apply(*args)
         return x
 
 

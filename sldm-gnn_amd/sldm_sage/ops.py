@@ -168,18 +168,25 @@ def scale_rows_by_inv_deg_(d: torch.Tensor, rowptr: torch.Tensor) -> torch.Tenso
 # ------------------------------------------------------------ dense (MFMA) --
 def sage_dense_fwd(agg: torch.Tensor, x: torch.Tensor, wcat: torch.Tensor, bias, gamma, beta,
                    eps: float, slope: float, drop_p: float, seed: int, save: bool,
-                   row_offset: int = 0):
+                   row_offset: int = 0, outs=None):
     """out = dropout(act(LN([agg|x]·wcat^T + bias))); returns (out, xhat|None, rstd|None).
 
-    wcat is [F_out, 2 F_in] (= [W_l | W_r]) in x's dtype."""
+    wcat is [F_out, 2 F_in] (= [W_l | W_r]) in x's dtype.  ``outs``: optional
+    preallocated (out, xhat, rstd), contiguous (row slices of bigger tensors)."""
     dev = _require_gpu(agg, x, wcat, gamma, beta, bias)
     n, fi = x.shape
     fo = wcat.size(0)
     assert agg.shape == x.shape and agg.stride(1) == 1 and x.stride(1) == 1
     assert wcat.is_contiguous() and wcat.shape == (fo, 2 * fi) and wcat.dtype == x.dtype
-    out = torch.empty(n, fo, dtype=x.dtype, device=dev)
-    xhat = torch.empty(n, fo, dtype=x.dtype, device=dev) if save else None
-    rstd = torch.empty(n, dtype=torch.float32, device=dev) if save else None
+    if outs is not None:
+        out, xhat, rstd = outs
+        assert out.is_contiguous() and out.shape == (n, fo) and out.dtype == x.dtype
+        assert (xhat is not None) == save and (rstd is not None) == save
+        assert not save or (xhat.is_contiguous() and rstd.is_contiguous())
+    else:
+        out = torch.empty(n, fo, dtype=x.dtype, device=dev)
+        xhat = torch.empty(n, fo, dtype=x.dtype, device=dev) if save else None
+        rstd = torch.empty(n, dtype=torch.float32, device=dev) if save else None
     f32 = lambda t: None if t is None else t.detach().float().contiguous()  # noqa: E731
     bias_, gamma_, beta_ = f32(bias), f32(gamma), f32(beta)
     s = x.element_size()

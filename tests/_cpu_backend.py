@@ -59,7 +59,18 @@ class CpuBackend:
         return x[idx.long()]
 
     @staticmethod
-    def layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p, seed, save, row_offset):
+    def layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p, seed, save, row_offset,
+                  outs=None):
+        res = CpuBackend._layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p)
+        if outs is None:
+            return res
+        for dst, src in zip(outs, res):
+            if dst is not None:
+                dst.copy_(src)
+        return outs
+
+    @staticmethod
+    def _layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p):
         assert drop_p == 0.0, "CPU test backend has no dropout"
         h = agg @ wl.detach().t() + bl.detach() + x @ wr.detach().t()
         mu = h.mean(1, keepdim=True)
