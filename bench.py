@@ -50,6 +50,7 @@ CONFIGS = {
 }
 ZIPF_A = 0.47   # dst rank ~ k^-a over N ranks: max in-degree ~ E*(2^(1-a)-1)/(N^(1-a)-1) ~ 10k at C5
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PMC_SUMMARY = "r1b_c4_pmc_traffic.json"   # latest committed PMC passes (tools/profile_round.sh)
 
 
 class KernelTimer:
@@ -284,7 +285,7 @@ def main():
     if g:
         achieved = g["avg_bytes"] / (g["avg_ms"] * 1e-3) / 1e9
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", "r1_c4_pmc_traffic.json")
+        pmc = os.path.join(ROOT, "profiles", PMC_SUMMARY)
         if (args.config == "c4" and args.graph == "uniform" and world == 1
                 and os.path.exists(pmc)):
             # HBM bytes per launch of this kernel at this workload, from the
@@ -293,7 +294,7 @@ def main():
                 traffic = int(json.load(fh)["gather_fwd_c4"]["hbm_bytes_per_launch"])
         roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
-                    traffic_unit=("bytes/launch (PMC, profiles/r1_c4_pmc_traffic.json)"
+                    traffic_unit=(f"bytes/launch (PMC, profiles/{PMC_SUMMARY})"
                                   if traffic is not None else
                                   "no PMC pass committed for this workload"),
                     kernel="gather_rows_kernel (forward mean aggregation)",
