@@ -107,7 +107,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
   constexpr int WSTAGE = WCOLS * 64;         // bytes per weight slice
   constexpr int WIPW = WCOLS / 128;          // weight DMA instructions per wave per k-step
   constexpr int VM_BASE = 2 * WIPW + 6;
-  constexpr int S_EPI = 32;                  // lower bound on epilogue vm ops per tile
+  // lower bound on epilogue vm ops per tile: LN 2 x 16 row stores (with
+  // xhat, see loose_ok), ROWSCALE 2 x NTT/2 paired 16-B stores
+  constexpr int S_EPI = MODE == ST_LN ? 32 : NTT;
   constexpr int VM_FIRST = VM_BASE + S_EPI > 63 ? 63 : VM_BASE + S_EPI;
   static_assert(KSTEPS % NSTW == 0 && KSTEPS % DA == 0 && KSTEPS >= NSTW, "ring shape");
   static_assert(MODE == ST_ROWSCALE || WN == 1, "LN needs the whole row in one wave");
@@ -200,8 +202,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
   }
 
   // The loose first-steps count is valid only when the previous epilogue
-  // issued >= S_EPI vm ops: always in ROWSCALE (32 stores), in LN only when
-  // xhat is written too (2 x 16 stores).
+  // issued >= S_EPI vm ops: always in ROWSCALE (NTT = 16 stores), in LN only
+  // when xhat is written too (2 x 16 stores).
   const bool loose_ok = MODE == ST_ROWSCALE || p.xhat != nullptr;
   bool first = true;
   for (;;) {
@@ -369,15 +371,34 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
         // 1/deg once per row (the 64-row kernels divide; the difference is
         // <= 1 fp32 ulp before the bf16 rounding)
         const float inv = HASDEG ? 1.0f / (float)(deg > 0 ? deg : 1) : 1.f;
+        // Tiles t, t+1 leave together as one 16-B store per lane: a lane
+        // holds 4 columns of each; v_permlane16_swap trades the odd row of
+        // the first operand with the even row of the second, so lanes of even
+        // q end with 8 contiguous columns of tile t (theirs + partner q+1's),
+        // lanes of odd q with 8 of tile t+1 (partner q-1's + theirs) -- half
+        // the store instructions of 8-B stores (store-issue-bound epilogue,
+        // MI355X_MICROARCH.md "epilogue store tail").
 #pragma unroll
-        for (int t = 0; t < NTT; ++t) {
-          const int c = wc * 256 + 16 * t + 4 * q;
-          // scale_cols (= F_in) is a multiple of 16: one uniform test per tile
-          const bool scaled = wc * 256 + 16 * t < p.scale_cols;
-          float v[4];
+        for (int t = 0; t < NTT; t += 2) {
+          uint32_t w[2][2];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = scaled ? acc[m][t][r] * inv : acc[m][t][r];
-          sldm::Vec<uint16_t, 4>::store(obase + row * p.ldo + c, v);
+          for (int h = 0; h < 2; ++h) {
+            // scale_cols (= F_in) is a multiple of 16: one uniform test per tile
+            const bool scaled = wc * 256 + 16 * (t + h) < p.scale_cols;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = scaled ? acc[m][t + h][r] * inv : acc[m][t + h][r];
+            w[h][0] = sldm::pack_bf16x2(v[0], v[1]);
+            w[h][1] = sldm::pack_bf16x2(v[2], v[3]);
+          }
+          uint4 o;
+          {
+            auto s0 = __builtin_amdgcn_permlane16_swap(w[0][0], w[1][0], false, false);
+            auto s1 = __builtin_amdgcn_permlane16_swap(w[0][1], w[1][1], false, false);
+            o = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+          }
+          const int c = wc * 256 + 16 * t + ((q & 1) ? 16 + 4 * (q - 1) : 4 * q);
+          *reinterpret_cast<uint4*>(obase + row * p.ldo + c) = o;
         }
       }
     }
@@ -453,7 +474,7 @@ bool stream_dense_fwd_ok(int64_t k0, int64_t K, int64_t nc, const void* a0, int6
 
 bool stream_rowscale_ok(int64_t k, int64_t nc, const void* a, int64_t lda, const void* b,
                         int64_t ldb, const void* out, int64_t ldo, int64_t scale_cols) {
-  return (nc == 256 || nc == 512) && ldo % 4 == 0 && scale_cols % 16 == 0 &&
+  return (nc == 256 || nc == 512) && ldo % 8 == 0 && scale_cols % 16 == 0 &&
          stream_common_ok(k, k, a, lda, a, lda, b, ldb) && aligned16(out);
 }
 
