@@ -163,6 +163,23 @@ int sldm_gemm_tn(int dtype, const void* a, int64_t lda, int64_t mo,
                  int64_t num_rows, float* out, void* workspace, size_t workspace_bytes,
                  void* stream);
 
+/* Fused layer boundary of the backward: the transpose gather of layer l
+ * (dx_l = addend + sum over out-edges of g, rows in row_order or 0..N-1)
+ * rounded to the storage type and fed straight into layer l-1's
+ * LayerNorm/activation/dropout backward (sldm_post_bwd's math, activation
+ * branch from fma(xhat, gamma, beta)): writes dh (same dtype) and column
+ * partials [num_partials][3][feat] for sldm_colsum.  Bit-identical dh to
+ * sldm_gather_rows + sldm_post_bwd with zout = NULL; dx_l never reaches HBM.
+ * Replaces the autograd of scatter_add_ / index_select (A8) of layer l and
+ * of Dropout/act/LayerNorm (sageblock.py:11-13) of layer l-1. */
+int sldm_gather_post_bwd_num_partials(int64_t num_rows, int64_t feat);
+int sldm_gather_post_bwd(int dtype, const void* g, int64_t ldg, const int32_t* t_rowptr,
+                         const int32_t* t_col, const int32_t* row_order, const void* addend,
+                         int64_t lda, int64_t num_rows, int64_t feat, const void* xhat,
+                         const float* rstd, const float* gamma, const float* beta,
+                         float negative_slope, float drop_p, uint64_t seed, int64_t row_offset,
+                         void* dh, float* col_partials, int num_partials, void* stream);
+
 /* ------------------------------------------------- graph-level readout ---
  * Global mean / max pooling over the batch vector:
  * replaces PyG 2.7.0 global_mean_pool / global_max_pool (grusage.py:3,

@@ -31,6 +31,13 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
 }
 
+// The value a float becomes once stored as T (bf16: rounded; fp32: itself).
+template <typename T> __device__ __forceinline__ float stored_value(float v);
+template <> __device__ __forceinline__ float stored_value<float>(float v) { return v; }
+template <> __device__ __forceinline__ float stored_value<uint16_t>(float v) {
+  return bf16_to_f32(f32_to_bf16(v));
+}
+
 // ------------------------------------------- vector load/store of V elems --
 // Loads V consecutive elements of T (float or uint16 bf16) into fp32 regs.
 template <typename T, int V> struct Vec;

@@ -34,11 +34,6 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kPoolPiece = 256;   // rows per piece (one row group each)
 
-template <typename T> __device__ __forceinline__ float stored_value(float v);
-template <> __device__ __forceinline__ float stored_value<float>(float v) { return v; }
-template <> __device__ __forceinline__ float stored_value<uint16_t>(float v) {
-  return sldm::bf16_to_f32(sldm::f32_to_bf16(v));
-}
 
 template <typename T, int V, int NCH>
 __global__ __launch_bounds__(kBlock) void pool_piece_kernel(
@@ -174,7 +169,7 @@ __global__ __launch_bounds__(kBlock) void pool_finish_kernel(
       // the divisor tests the stored (dtype-rounded) max against 0, as torch does
 #pragma unroll
       for (int v = 0; v < V; ++v)
-        ndist[seg * (int64_t)feat + f + v] = n[v] + (stored_value<T>(mx[v]) == 0.f ? 1.f : 0.f);
+        ndist[seg * (int64_t)feat + f + v] = n[v] + (sldm::stored_value<T>(mx[v]) == 0.f ? 1.f : 0.f);
     }
     if (argmax) {
 #pragma unroll

@@ -92,6 +92,10 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
     int64_t nrows, int feat, int lpr_log2, const float* __restrict__ gamma,
     const float* __restrict__ beta, float slope, float drop_p, float drop_scale, uint64_t seed, int64_t row_off,
     TD* __restrict__ dh, float* __restrict__ partials) {
+  // Contraction off: every product rounds on its own and the fmas are the
+  // explicit ones, so gather_post.hip's fused copy of this math gives the
+  // same bits whatever the compiler fuses in either kernel.
+#pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) float red[];  // [kBlock/lpr][3][feat] reused
   const int lpr = 1 << lpr_log2;
   const int lane_in_row = threadIdx.x & (lpr - 1);
@@ -171,7 +175,7 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
           dy[c][k] = d;
           gx[c][k] = d * g;
           s1 += gx[c][k];
-          s2 += gx[c][k] * xh[u][c][k];
+          s2 = __builtin_fmaf(gx[c][k], xh[u][c][k], s2);
         }
       }
       const float m1 = group_sum(s1, lpr) * inv_f;
@@ -183,8 +187,8 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
         float o[V];
 #pragma unroll
         for (int k = 0; k < V; ++k) {
-          o[k] = rs * (gx[c][k] - m1 - xh[u][c][k] * m2);
-          pg[c][k] += dy[c][k] * xh[u][c][k];
+          o[k] = rs * __builtin_fmaf(-xh[u][c][k], m2, gx[c][k] - m1);
+          pg[c][k] = __builtin_fmaf(dy[c][k], xh[u][c][k], pg[c][k]);
           pb[c][k] += dy[c][k];
           pd[c][k] += o[k];
         }

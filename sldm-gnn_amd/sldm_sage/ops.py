@@ -268,6 +268,39 @@ def post_fwd(h: torch.Tensor, bias, gamma, beta, eps: float, slope: float, drop_
     return out, xhat, rstd
 
 
+def gather_post_bwd(g: torch.Tensor, t_rowptr: torch.Tensor, t_col: torch.Tensor,
+                    t_order: torch.Tensor | None, addend: torch.Tensor, xhat: torch.Tensor,
+                    rstd: torch.Tensor, gamma, beta, slope: float, drop_p: float, seed: int,
+                    row_offset: int = 0):
+    """Fused layer boundary of the backward (gather_post.hip): the transpose
+    gather of layer l (+ its root-path ``addend``) fed straight into layer
+    l-1's LayerNorm/act/dropout backward.  Returns (dh, dgamma, dbeta, dbias)
+    of layer l-1, as :func:`post_bwd` would from the gathered gradient."""
+    dev = _require_gpu(g, t_rowptr, t_col, t_order, addend, xhat, rstd)
+    N, F = xhat.shape
+    assert g.dtype == xhat.dtype == addend.dtype and g.stride(1) == 1 and addend.stride(1) == 1
+    assert xhat.is_contiguous() and g.size(1) == F and addend.shape == (N, F)
+    lib = _lib.load()
+    np_ = lib.sldm_gather_post_bwd_num_partials(N, F)
+    dh = torch.empty(N, F, dtype=xhat.dtype, device=dev)
+    partials = torch.empty(np_, 3 * F, dtype=torch.float32, device=dev)
+    cols = torch.empty(3 * F, dtype=torch.float32, device=dev)
+    gamma_ = gamma.detach().float().contiguous()
+    beta_ = beta.detach().float().contiguous()
+    s = xhat.element_size()
+    E = t_col.numel()
+    with _Timed("gather_post_bwd", E * (4 + F * s) + (N + 1) * 4 + 3 * N * F * s + 4 * N):
+        _lib.check(lib.sldm_gather_post_bwd(
+            dtype_code(xhat), g.data_ptr(), g.stride(0), t_rowptr.data_ptr(),
+            t_col.data_ptr() if E else t_rowptr.data_ptr(), _ptr(t_order), addend.data_ptr(),
+            addend.stride(0), N, F, xhat.data_ptr(), rstd.data_ptr(), gamma_.data_ptr(),
+            beta_.data_ptr(), float(slope), float(drop_p), seed & (2**64 - 1), int(row_offset),
+            dh.data_ptr(), partials.data_ptr(), np_, _stream(dev)), "sldm_gather_post_bwd")
+        _lib.check(lib.sldm_colsum(partials.data_ptr(), np_, 3 * F, cols.data_ptr(),
+                                   _stream(dev)), "sldm_colsum")
+    return dh, cols[:F], cols[F:2 * F], cols[2 * F:]
+
+
 def branch_source(out: torch.Tensor) -> torch.Tensor | None:
     """What the post backward reads to pick the activation branch.
 

@@ -96,6 +96,77 @@ class _SageLayerFn(torch.autograd.Function):
                 dgamma.to(gamma.dtype), dbeta.to(beta.dtype), None, None, None, None, None)
 
 
+# Training runs the stack as one autograd node with fused layer boundaries
+# (_SageStackFn); False (or SLDM_FUSE_BOUNDARIES=0) selects one node per layer
+# (_SageLayerFn) -- same results, for A/B comparisons and the tests.
+FUSE_BOUNDARIES = __import__("os").environ.get("SLDM_FUSE_BOUNDARIES", "1") != "0"
+
+
+class _SageStackFn(torch.autograd.Function):
+    """All layers of a SageBlock as one autograd node, so the backward can fuse
+    each layer boundary: the transpose gather of layer l and the LayerNorm /
+    act / dropout backward of layer l-1 run as one kernel (gather_post.hip)
+    and the input gradient of layer l never reaches HBM.  Forward and every
+    per-layer operation are those of :class:`_SageLayerFn`; the results are
+    bit-identical to it (dh from the fused kernel equals post_bwd of the
+    gathered gradient; only the fp32 column sums of dgamma / dbeta / dbias are
+    summed in a different row order)."""
+
+    @staticmethod
+    def forward(ctx, x, graph: SageGraph, cfgs, *params):
+        n = x.size(0)
+        saved = []
+        h = x
+        for i, (slope, drop_p, seed, eps) in enumerate(cfgs):
+            wl, bl, wr, gamma, beta = params[5 * i: 5 * i + 5]
+            agg = ops.gather_rows(h, graph.rowptr, graph.col, n, mean=True, name="gather_fwd",
+                                  order=graph.order)
+            out, xhat, rstd = dense.sage_layer_fwd(agg, h, wl, bl, wr, gamma, beta, eps, slope,
+                                                   drop_p, seed, save=True)
+            saved += [h, agg, xhat, rstd]
+            h = out
+        ctx.save_for_backward(*saved, *params)
+        ctx.graph, ctx.cfgs, ctx.nl = graph, cfgs, len(cfgs)
+        return h
+
+    @staticmethod
+    def backward(ctx, dout):
+        nl, graph, cfgs = ctx.nl, ctx.graph, ctx.cfgs
+        st = ctx.saved_tensors
+        acts, params = st[: 4 * nl], st[4 * nl:]
+        if graph.t_rowptr is None:
+            raise RuntimeError("SageGraph was built without its transpose; rebuild with "
+                               "transpose=True for backward")
+        grads = [None] * len(params)
+        x_in = acts[0]
+        top = nl - 1
+        slope, drop_p, seed, _ = cfgs[top]
+        wl, bl, wr, gamma, beta = params[5 * top: 5 * top + 5]
+        dh, dgamma, dbeta, dbl = ops.post_bwd(dout, acts[4 * top + 2], acts[4 * top + 3], gamma,
+                                              beta, slope, drop_p, seed, dh_dtype=x_in.dtype)
+        dx = None
+        for i in range(top, -1, -1):
+            h, agg = acts[4 * i], acts[4 * i + 1]
+            wl, bl, wr, gamma, beta = params[5 * i: 5 * i + 5]
+            dwl, dwr = dense.sage_linear_bwd_weight(dh, agg, h)
+            grads[5 * i: 5 * i + 5] = [dwl.to(wl.dtype), dbl.to(wl.dtype), dwr.to(wr.dtype),
+                                       dgamma.to(gamma.dtype), dbeta.to(beta.dtype)]
+            if i == 0 and not ctx.needs_input_grad[0]:
+                break
+            g, dx_r = dense.sage_linear_bwd_data(dh, wl, wr, graph.rowptr)
+            if i == 0:
+                dx = ops.gather_rows(g, graph.t_rowptr, graph.t_col, h.size(0), mean=False,
+                                     order=graph.t_order, addend=dx_r, name="gather_bwd")
+                break
+            # boundary: layer i's input gradient straight into layer i-1's post backward
+            slope, drop_p, seed, _ = cfgs[i - 1]
+            gamma_b, beta_b = params[5 * (i - 1) + 3], params[5 * (i - 1) + 4]
+            dh, dgamma, dbeta, dbl = ops.gather_post_bwd(
+                g, graph.t_rowptr, graph.t_col, graph.t_order, dx_r, acts[4 * (i - 1) + 2],
+                acts[4 * (i - 1) + 3], gamma_b, beta_b, slope, drop_p, seed)
+        return (dx, None, None, *grads)
+
+
 class SageConv(nn.Module):
     """Parameter layout of PyG 2.7.0 ``SAGEConv(in, out)`` with default arguments
     (aggr='mean', root_weight=True, bias=True, normalize=False, project=False),
@@ -180,12 +251,20 @@ class SageBlock(nn.Module):
         if x.dtype not in (torch.float32, torch.bfloat16):
             x = x.float()
         x = x.contiguous()
+        layers = []
         for conv, post in zip(self.convs, self.posts):
             ln, act, drop = post[0], post[1], post[2]
             if not isinstance(ln, nn.LayerNorm) or ln.weight is None:
                 raise TypeError("SageBlock post[0] must be an affine LayerNorm")
             p = _drop_p(drop)
-            x = _SageLayerFn.apply(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight,
-                                   ln.weight, ln.bias, graph, _act_slope(act), p,
-                                   _new_seed() if p > 0 else 0, float(ln.eps))
+            layers.append(((conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, ln.weight,
+                            ln.bias), (_act_slope(act), p, _new_seed() if p > 0 else 0,
+                                       float(ln.eps))))
+        if grad and FUSE_BOUNDARIES and ops.branch_source(x) is None:
+            # training: one autograd node for the stack (fused layer boundaries)
+            cfgs = tuple(c for _, c in layers)
+            params = [t for w, _ in layers for t in w]
+            return _SageStackFn.apply(x, graph, cfgs, *params)
+        for (wl, bl, wr, gamma, beta), (slope, p, seed, eps) in layers:
+            x = _SageLayerFn.apply(x, wl, bl, wr, gamma, beta, graph, slope, p, seed, eps)
         return x

