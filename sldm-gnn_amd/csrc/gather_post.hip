@@ -67,11 +67,26 @@ __global__ __launch_bounds__(kBlock) void gather_post_bwd_kernel(
   const int64_t stride = (int64_t)gridDim.x * groups_per_block;
   const int64_t nrounds = (nrows + stride - 1) / stride;
 
-  for (int64_t it = 0; it < nrounds; ++it) {
+  // row of iteration `it` and its CSR range, one iteration ahead: the next
+  // row's rowptr loads are in flight while this row is gathered
+  auto row_of = [&](int64_t it, bool& live) -> int64_t {
     const int64_t slot = it * stride + (int64_t)blockIdx.x * groups_per_block + group;
-    const bool live = slot < nrows;
+    live = slot < nrows;
     const int64_t s = live ? slot : 0;
-    const int64_t row = order ? (int64_t)order[s] : s;
+    return order ? (int64_t)order[s] : s;
+  };
+  bool live_n;
+  int64_t row_n = row_of(0, live_n);
+  int beg_n = t_rowptr[row_n], end_n = t_rowptr[row_n + 1];
+  for (int64_t it = 0; it < nrounds; ++it) {
+    const bool live = live_n;
+    const int64_t row = row_n;
+    const int beg = beg_n, end = end_n;
+    if (it + 1 < nrounds) {
+      row_n = row_of(it + 1, live_n);
+      beg_n = t_rowptr[row_n];
+      end_n = t_rowptr[row_n + 1];
+    }
 
     // xhat / rstd of the row first: in flight beside the gather
     float xh[NCH][V];
@@ -85,7 +100,6 @@ __global__ __launch_bounds__(kBlock) void gather_post_bwd_kernel(
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
       for (int v = 0; v < V; ++v) acc[c][v] = 0.f;
-    const int beg = t_rowptr[row], end = t_rowptr[row + 1];
     auto batch = [&](int k, auto u_const) {
       constexpr int U = decltype(u_const)::value;
       int idx[U];
