@@ -426,6 +426,9 @@ int launch_nt(NtArgs<T>& p, hipStream_t stream) {
 }
 
 // ------------------------------------------------------------------- TN --
+#ifndef SLDM_TN_BK
+#define SLDM_TN_BK 32
+#endif
 template <typename T>
 struct TnArgs {
   const T* a; int64_t lda; int mo;             // A [rows][mo]
@@ -437,7 +440,7 @@ struct TnArgs {
   float* slab;                                 // [splits][mo][nn]
 };
 
-constexpr int TN_BK = 32;    // node rows per k-step
+constexpr int TN_BK = SLDM_TN_BK;   // node rows per k-step (32 | 64)
 constexpr int TN_TILE = 128; // block tile (m and n)
 
 template <typename T> struct TnLds {
@@ -547,9 +550,11 @@ __global__ __launch_bounds__(kBlock) void gemm_tn_kernel(TnArgs<T> p) {
       sb.load(elem_b, k0 + TN_BK, nbase, kend, p.nn);
     }
     if constexpr (sizeof(T) == 2) {
+#pragma unroll
+     for (int kb = 0; kb < TN_BK; kb += 32) {
       // Lane 4i+j of a 16-lane group addresses row (8q + i), columns 4j..4j+3
       // of a 4x16 block; it receives column r16 of rows 8q..8q+3 (T10).
-      const int rr = 8 * q + (r16 >> 2);
+      const int rr = kb + 8 * q + (r16 >> 2);
       const int cc = 4 * (r16 & 3);
       s8v af[4], bf[4];
 #pragma unroll
@@ -571,6 +576,7 @@ __global__ __launch_bounds__(kBlock) void gemm_tn_kernel(TnArgs<T> p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+     }
     } else {
 #pragma unroll
       for (int kk = 0; kk < TN_BK; kk += 4) {
@@ -624,7 +630,16 @@ TnPlan tn_plan(int64_t rows, int64_t mo, int64_t nn) {
   pl.tiles_m = (int)((mo + TN_TILE - 1) / TN_TILE);
   pl.tiles_n = (int)((nn + TN_TILE - 1) / TN_TILE);
   const int tiles = pl.tiles_m * pl.tiles_n;
-  int64_t splits = 512 / tiles;                       // ~2 blocks per CU
+  // ~3 resident blocks per CU (the kernel runs 3 waves per SIMD) on long node
+  // dimensions; the SLDM_TN_BLOCKS environment variable overrides (A/B runs)
+  static const int64_t target = [] {
+    const char* e = getenv("SLDM_TN_BLOCKS");
+    const long v = e ? atol(e) : 0;
+    return (int64_t)(v > 0 ? v : 0);
+  }();
+  // 768 measured best at C4 (10M rows: 4.63 -> 3.84 ms vs 512); short node
+  // dimensions keep 512 (C2: the extra slabs cost more than they hide)
+  int64_t splits = (target ? target : (rows >= 2000000 ? 768 : 512)) / tiles;
   const int64_t max_splits = (rows + 8 * TN_BK - 1) / (8 * TN_BK);  // >= 8 k-steps each
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
