@@ -180,6 +180,18 @@ int sldm_gather_post_bwd(int dtype, const void* g, int64_t ldg, const int32_t* t
                          float negative_slope, float drop_p, uint64_t seed, int64_t row_offset,
                          void* dh, float* col_partials, int num_partials, void* stream);
 
+/* ------------------------------------------ multi-GPU layout switches ---
+ * Feature-sliced SageBlock (sldm_sage/dist.py): rows [num_rows, B*bc] (row
+ * stride ld_rows) <-> B column blocks [B][num_rows][bc] (contiguous), the
+ * buffers the all-to-alls send / receive.  unpack optionally adds a
+ * row-layout addend (dx = dx_root + gathered dAgg gradient, one rounding).
+ * bc must be a multiple of 16 bytes' worth of elements. */
+int sldm_cols_pack(int dtype, const void* rows_src, int64_t ld_rows, int64_t num_rows,
+                   int64_t num_blocks, int64_t block_cols, void* blocks_dst, void* stream);
+int sldm_cols_unpack(int dtype, const void* blocks_src, int64_t num_rows, int64_t num_blocks,
+                     int64_t block_cols, const void* addend, int64_t ld_add, void* rows_dst,
+                     int64_t ld_rows, void* stream);
+
 /* ------------------------------------------------- graph-level readout ---
  * Global mean / max pooling over the batch vector:
  * replaces PyG 2.7.0 global_mean_pool / global_max_pool (grusage.py:3,

@@ -60,6 +60,10 @@ _SIGNATURES = {
                                             _c_i64, _c_i64, _vp, _vp, _vp, _vp, ctypes.c_float,
                                             ctypes.c_float, ctypes.c_uint64, _c_i64, _vp, _vp,
                                             ctypes.c_int, _vp]),
+    "sldm_cols_pack": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _vp,
+                                      _vp]),
+    "sldm_cols_unpack": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64,
+                                        _vp, _c_i64, _vp]),
     "sldm_segment_pool_piece_rows": (ctypes.c_int, []),
     "sldm_segment_pool_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
     "sldm_segment_pool": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _vp, _vp, _c_i64, _vp,

@@ -119,6 +119,27 @@ class HipBackend:
         from . import dense
         return dense.sage_linear_bwd_weight(dh, agg, x)
 
+    @staticmethod
+    def cols_pack(rows, nblk, cs):
+        """rows [n, nblk*cs] -> flat [nblk][n][cs] (layout.hip; torch for odd widths)."""
+        from . import ops
+        if ops.cols_layout_ok(rows, cs) and rows.stride(1) == 1:
+            return ops.cols_pack(rows, nblk, cs)
+        return rows.reshape(rows.size(0), nblk, cs).transpose(0, 1).contiguous().view(-1)
+
+    @staticmethod
+    def cols_unpack(blocks, n, nblk, cs, out, addend=None):
+        """flat [nblk][n][cs] -> out [n, nblk*cs] (+ addend)."""
+        from . import ops
+        if ops.cols_layout_ok(out, cs):
+            return ops.cols_unpack(blocks, n, nblk, cs, out, addend)
+        src = blocks.view(nblk, n, cs).transpose(0, 1).reshape(n, nblk * cs)
+        if addend is None:
+            out.copy_(src)
+        else:
+            torch.add(addend, src, out=out)
+        return out
+
 
 @dataclass
 class HaloPlan:
@@ -411,7 +432,7 @@ def _a2a(out, inp, out_splits, in_splits, group):
 
 
 def _rows_to_cols(part: FeaturePartition, src: torch.Tensor, j: int, dst_cols: torch.Tensor,
-                  group):
+                  group, backend):
     """Chunk j of this rank's rows of ``src`` [n_own, F] -> rows
     [chunk_start[j], chunk_start[j+1]) of the column-sliced ``dst_cols``
     [N, F_r] on every rank.  Returns (work, keep-alive)."""
@@ -423,7 +444,7 @@ def _rows_to_cols(part: FeaturePartition, src: torch.Tensor, j: int, dst_cols: t
         return None, None
     rows = b - a
     if all(c == cs[0] for c in cs):
-        send = src[a:b].reshape(rows, W, cs[0]).transpose(0, 1).contiguous()
+        send = backend.cols_pack(src[a:b], W, cs[0]) if rows else src.new_empty(0)
     else:
         send = torch.cat([src[a:b, sum(cs[:c]): sum(cs[:c + 1])].reshape(-1)
                           for c in range(W)]) if rows else src.new_empty(0)
@@ -449,18 +470,27 @@ def _cols_to_rows(part: FeaturePartition, src_cols: torch.Tensor, j: int, feat: 
     return work, recv, cs
 
 
-def _cols_to_rows_finish(part, recv, cs, rows, out_rows):
-    """Interleave the per-rank column blocks of ``recv`` into ``out_rows`` [rows, F]."""
+def _cols_to_rows_finish(part, recv, cs, rows, out_rows, backend, addend=None):
+    """Interleave the per-rank column blocks of ``recv`` into ``out_rows``
+    [rows, F] (+ ``addend`` rows, one rounding)."""
+    if rows == 0:
+        return
     if part.world == 1:
-        out_rows.copy_(recv)
+        if addend is None:
+            out_rows.copy_(recv)
+        else:
+            torch.add(addend, recv, out=out_rows)
         return
     if all(c == cs[0] for c in cs):
-        out_rows.view(rows, part.world, cs[0]).copy_(
-            recv.view(part.world, rows, cs[0]).transpose(0, 1))
+        backend.cols_unpack(recv, rows, part.world, cs[0], out_rows, addend)
         return
     off, col = 0, 0
     for c in cs:
-        out_rows[:, col:col + c].copy_(recv[off: off + rows * c].view(rows, c))
+        piece = recv[off: off + rows * c].view(rows, c)
+        if addend is None:
+            out_rows[:, col:col + c].copy_(piece)
+        else:
+            torch.add(addend[:, col:col + c], piece, out=out_rows[:, col:col + c])
         off += rows * c
         col += c
 
@@ -473,9 +503,10 @@ def _feat_gather(backend, src_cols, rowptr, col, part, j, mean, out_cols, edges)
 
 
 def _feat_aggregate_to_rows(backend, part, src_cols, rowptr, col, mean, feat, chunk_edges,
-                            group):
+                            group, addend=None):
     """Aggregate all rows over this rank's columns, chunk by chunk, and bring
-    each finished chunk back to row layout while the next chunk is gathered."""
+    each finished chunk back to row layout while the next chunk is gathered
+    (+ ``addend`` rows: the backward's root-path gradient)."""
     out_cols = src_cols.new_empty(part.num_nodes, src_cols.size(1))
     out_rows = src_cols.new_empty(part.num_rows, feat)
     pending = []
@@ -486,18 +517,19 @@ def _feat_aggregate_to_rows(backend, part, src_cols, rowptr, col, mean, feat, ch
         if work is not None:
             work.wait()
         a, b = part.own_chunk[j], part.own_chunk[j + 1]
-        _cols_to_rows_finish(part, recv, cs, b - a, out_rows[a:b])
+        _cols_to_rows_finish(part, recv, cs, b - a, out_rows[a:b], backend,
+                             addend[a:b] if addend is not None else None)
     return out_rows
 
 
-def _feat_rows_to_cols(part, x_rows, group):
+def _feat_rows_to_cols(part, x_rows, group, backend):
     """Column-sliced copy [N, F_r] of the row-partitioned ``x_rows``; returns
     (buffer, works) -- wait on every work before reading the buffer."""
     cs = part.col_sizes(x_rows.size(1))
     buf = x_rows.new_empty(part.num_nodes, cs[part.rank])
     works = []
     for j in range(part.num_chunks):
-        w, keep = _rows_to_cols(part, x_rows, j, buf, group)
+        w, keep = _rows_to_cols(part, x_rows, j, buf, group, backend)
         if w is not None:
             works.append((w, keep))
     return buf, works
@@ -523,7 +555,8 @@ class _FeatLayerFn(torch.autograd.Function):
         F = x.size(1)
         fo = wl.size(0)
         pre = carry.pop("cols", None)
-        x_cols, works = pre if pre is not None else _feat_rows_to_cols(part, x, group)
+        x_cols, works = pre if pre is not None else _feat_rows_to_cols(part, x, group,
+                                                                        backend)
         _wait_all(works)
         out_cols = x_cols.new_empty(part.num_nodes, x_cols.size(1))
         pending = []
@@ -545,14 +578,14 @@ class _FeatLayerFn(torch.autograd.Function):
             a, b = part.own_chunk[j], part.own_chunk[j + 1]
             if work is not None:
                 work.wait()
-            _cols_to_rows_finish(part, recv, cs_in, b - a, agg[a:b])
+            _cols_to_rows_finish(part, recv, cs_in, b - a, agg[a:b], backend)
             if b > a:
                 backend.layer_fwd(agg[a:b], x[a:b], wl, bl, wr, gamma, beta, eps, slope, drop_p,
                                   seed, save, part.row_begin + a,
                                   outs=(out[a:b], xhat[a:b] if save else None,
                                         rstd[a:b] if save else None))
             if nxt is not None:
-                w, keep = _rows_to_cols(part, out, j, nxt[0], group)
+                w, keep = _rows_to_cols(part, out, j, nxt[0], group, backend)
                 if w is not None:
                     nxt[1].append((w, keep))
         del x_cols, out_cols, pending
@@ -575,7 +608,7 @@ class _FeatLayerFn(torch.autograd.Function):
                                              drop_p, seed, out, part.row_begin)
         g, dx_r = be.bwd_data(dh, wl, wr, part.own_rowptr)
         # dAgg/deg to column layout (RCCL stream) while the weight-grad GEMM runs
-        g_cols, works = _feat_rows_to_cols(part, g, group)
+        g_cols, works = _feat_rows_to_cols(part, g, group, be)
         dwl, dwr = be.bwd_weight(dh, agg, x)
         grads = (dwl, dbl, dwr, dgamma, dbeta)
         flat = torch.cat([t.reshape(-1).float() for t in grads])
@@ -583,9 +616,9 @@ class _FeatLayerFn(torch.autograd.Function):
         if part.world > 1:
             rwork = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group, async_op=True)
         _wait_all(works)
-        dxa = _feat_aggregate_to_rows(be, part, g_cols, gr.t_rowptr, gr.t_col, False, F,
-                                      part.chunk_t_edges, group)
-        dx = dx_r + dxa
+        # dx = dx_root + the gathered gradient, added as the blocks are unpacked
+        dx = _feat_aggregate_to_rows(be, part, g_cols, gr.t_rowptr, gr.t_col, False, F,
+                                     part.chunk_t_edges, group, addend=dx_r.contiguous())
         if rwork is not None:
             rwork.wait()
         dwl, dbl, dwr, dgamma, dbeta = (c.view_as(t) for c, t in zip(

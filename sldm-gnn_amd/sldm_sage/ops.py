@@ -301,6 +301,41 @@ def gather_post_bwd(g: torch.Tensor, t_rowptr: torch.Tensor, t_col: torch.Tensor
     return dh, cols[:F], cols[F:2 * F], cols[2 * F:]
 
 
+def cols_layout_ok(t: torch.Tensor, block_cols: int) -> bool:
+    """Whether :func:`cols_pack` / :func:`cols_unpack` take this dtype / width."""
+    return t.dtype in _DTYPE_CODE and (block_cols * t.element_size()) % 16 == 0
+
+
+def cols_pack(rows: torch.Tensor, num_blocks: int, block_cols: int,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """rows [n, B*bc] -> flat [B][n][bc] (layout.hip)."""
+    dev = _require_gpu(rows, out)
+    n = rows.size(0)
+    assert rows.size(1) == num_blocks * block_cols and rows.stride(1) == 1
+    if out is None:
+        out = torch.empty(num_blocks * n * block_cols, dtype=rows.dtype, device=dev)
+    with _Timed("cols_pack", 2 * rows.numel() * rows.element_size()):
+        _lib.check(_lib.load().sldm_cols_pack(dtype_code(rows), rows.data_ptr(), rows.stride(0),
+                                              n, num_blocks, block_cols, out.data_ptr(),
+                                              _stream(dev)), "sldm_cols_pack")
+    return out
+
+
+def cols_unpack(blocks: torch.Tensor, num_rows: int, num_blocks: int, block_cols: int,
+                out: torch.Tensor, addend: torch.Tensor | None = None) -> torch.Tensor:
+    """flat [B][n][bc] -> out [n, B*bc] (+ addend, one rounding) (layout.hip)."""
+    dev = _require_gpu(blocks, out, addend)
+    assert out.shape == (num_rows, num_blocks * block_cols) and out.stride(1) == 1
+    if addend is not None:
+        assert addend.shape == out.shape and addend.stride(1) == 1 and addend.dtype == out.dtype
+    with _Timed("cols_unpack", (2 + (addend is not None)) * out.numel() * out.element_size()):
+        _lib.check(_lib.load().sldm_cols_unpack(
+            dtype_code(out), blocks.data_ptr(), num_rows, num_blocks, block_cols, _ptr(addend),
+            addend.stride(0) if addend is not None else 0, out.data_ptr(), out.stride(0),
+            _stream(dev)), "sldm_cols_unpack")
+    return out
+
+
 def branch_source(out: torch.Tensor) -> torch.Tensor | None:
     """What the post backward reads to pick the activation branch.
 

@@ -96,3 +96,16 @@ class CpuBackend:
     @staticmethod
     def bwd_weight(dh, agg, x):
         return dh.t() @ agg, dh.t() @ x
+
+    @staticmethod
+    def cols_pack(rows, nblk, cs):
+        return rows.reshape(rows.size(0), nblk, cs).transpose(0, 1).contiguous().view(-1)
+
+    @staticmethod
+    def cols_unpack(blocks, n, nblk, cs, out, addend=None):
+        src = blocks.view(nblk, n, cs).transpose(0, 1).reshape(n, nblk * cs)
+        if addend is None:
+            out.copy_(src)
+        else:
+            torch.add(addend, src, out=out)
+        return out

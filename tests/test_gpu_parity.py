@@ -684,3 +684,20 @@ def test_stack_fused_backward_equals_per_layer(dtype, hd):
             assert torch.equal(pa[k], pb[k]), k
         else:
             torch.testing.assert_close(pa[k], pb[k], atol=1e-3, rtol=1e-4)
+
+
+# ------------------------------------------------------ multi-GPU layout ops --
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,nblk,cs", [(1000, 8, 32), (777, 4, 64), (5, 2, 128), (0, 8, 32)])
+def test_cols_pack_unpack_match_torch(dtype, n, nblk, cs):
+    from sldm_sage import ops
+    gen = torch.Generator(device=DEV).manual_seed(n + cs)
+    rows = torch.randn(n, nblk * cs, generator=gen, device=DEV).to(dtype)
+    packed = ops.cols_pack(rows, nblk, cs)
+    assert torch.equal(packed, rows.reshape(n, nblk, cs).transpose(0, 1).contiguous().view(-1))
+    out = torch.empty_like(rows)
+    ops.cols_unpack(packed, n, nblk, cs, out)
+    assert torch.equal(out, rows)
+    add = torch.randn(n, nblk * cs, generator=gen, device=DEV).to(dtype)
+    ops.cols_unpack(packed, n, nblk, cs, out, addend=add)
+    assert torch.equal(out, add + rows)
