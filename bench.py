@@ -131,6 +131,9 @@ def cpu_baseline(cfg, threads):
 
 
 def _parallelism(strategy, world):
+    if strategy == "replicate":
+        return (f"replicated x{world} (the planner found no partition of this graph faster "
+                "than one GPU doing all the work: every rank runs the whole block)")
     if strategy == "feature":
         return f"feature-sliced x{world} (all rows, F/{world} columns per rank), RCCL all-to-all"
     return f"dst-partition x{world}, RCCL halo all-to-all"
@@ -149,7 +152,8 @@ def main():
                          "in-degrees (default for c5)")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the partitioned (multi-GPU) path even on one GPU")
-    ap.add_argument("--strategy", default="auto", choices=["auto", "halo", "feature"],
+    ap.add_argument("--strategy", default="auto",
+                    choices=["auto", "halo", "feature", "replicate"],
                     help="multi-GPU partition: destination rows + halo exchange, feature "
                          "slices + layout all-to-alls, or the lower modelled time (default)")
     args = ap.parse_args()
@@ -200,7 +204,7 @@ def main():
             dist_info = {"strategy": plan["strategy"],
                          "exchange_bytes_per_layer_rank0":
                              part.exchange_bytes_per_layer(f, x.element_size())}
-            for k in ("halo_s", "feature_s"):
+            for k in ("halo_s", "feature_s", "replicate_s"):
                 if k in plan:
                     dist_info[f"model_{k[:-2]}_ms_per_layer"] = round(plan[k] * 1e3, 3)
             if plan["strategy"] == "halo":
@@ -219,7 +223,7 @@ def main():
                                   "cross_partition_edge_fraction_rank0": round(cross, 4),
                                   "overlap_resident_rows_fwd_rank0": resident(part.fwd_split),
                                   "overlap_resident_rows_bwd_rank0": resident(part.bwd_split)})
-            else:
+            elif plan["strategy"] == "feature":
                 dist_info["chunks"] = part.num_chunks
             del ei, x, gout
             torch.cuda.empty_cache()

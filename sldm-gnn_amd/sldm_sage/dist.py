@@ -45,7 +45,10 @@ Per layer a rank moves 4 x (W-1)/W^2 x N x F x s bytes, against
 load is balanced by construction (power-law in-degrees included) and each
 element is still summed in CSR order (fp32: bit-identical to one GPU; bf16:
 the backward's two-term add rounds once more).  :func:`plan_partition`
-picks the strategy with the lower modelled time.
+picks the strategy with the lowest modelled time -- including *replicate*
+(no sharding, every rank runs the whole block) for graphs where any
+partition would move more bytes over xGMI than one GPU needs to do all the
+work (a uniform random graph at W = 2: one link per peer).
 
 The per-rank compute goes through a backend object (default: the HIP ops);
 the CPU tests plug a plain-torch backend in to run the same protocol over
@@ -698,10 +701,16 @@ class DistSageBlock(nn.Module):
 
     @property
     def strategy(self) -> str:
+        if isinstance(self.part, ReplicaPartition):
+            return "replicate"
         return "feature" if isinstance(self.part, FeaturePartition) else "halo"
 
     def forward(self, x_local: torch.Tensor) -> torch.Tensor:
         from .sageblock import _act_slope, _drop_p, _new_seed
+        if isinstance(self.part, ReplicaPartition):
+            # every rank runs the whole block: gradients are complete and
+            # identical on every rank, nothing crosses xGMI
+            return self.block(x_local, self.part.graph)
         feat = isinstance(self.part, FeaturePartition)
         x = x_local.contiguous()
         layers = list(zip(self.block.convs, self.block.posts))
@@ -746,10 +755,19 @@ def _remote_unique(ids: torch.Tensor, r0: int, r1: int) -> int:
     return int(((u < r0) | (u >= r1)).sum())
 
 
+# dense part (fwd GEMM + LN, LN backward, dX, dW) per layer and row, in units
+# of F*s bytes at the stream kernels' measured rate (§4: ~13 F s per row)
+_DENSE_BYTES_PER_ROW_FS = 13.0
+_DENSE_BPS = 4.0e12
+_FEAT_CHUNKS = 4          # partition_features' default pipeline depth
+
+
 def estimate_strategies(edge_index: torch.Tensor, num_nodes: int, world: int, rank: int,
                         feat: int, elem: int, group=None) -> dict:
-    """Modelled per-layer time (s) of the halo and feature-sliced strategies,
-    max over ranks (collective over ``group`` when world > 1)."""
+    """Modelled per-layer time (s) of the halo, feature-sliced and replicated
+    strategies: exchange bytes / xGMI + gather bytes / measured gather rate +
+    dense bytes / stream rate, max over ranks (collective over ``group`` when
+    world > 1, so every rank gets the same numbers)."""
     P = (num_nodes + world - 1) // world
     r0, r1 = min(rank * P, num_nodes), min((rank + 1) * P, num_nodes)
     src, dst = edge_index[0], edge_index[1]
@@ -760,37 +778,86 @@ def estimate_strategies(edge_index: torch.Tensor, num_nodes: int, world: int, ra
     e_in, e_out = int(in_mask.sum()), int(out_mask.sum())
     link = max(world - 1, 1) * _LINK_BPS
     row = feat * elem
+    dense_own = _DENSE_BYTES_PER_ROW_FS * (r1 - r0) * row / _DENSE_BPS
     halo_t = ((halo_f + halo_b) * row / link
-              + (e_in + e_out) * (row + 4) / _gather_rate(row))
+              + (e_in + e_out) * (row + 4) / _gather_rate(row) + dense_own)
     fc = max(1, feat // world)
     e = int(edge_index.size(1))
-    feat_t = (4 * (world - 1) * (r1 - r0) * fc * elem / link
-              + 2 * e * (fc * elem + 4) / _gather_rate(fc * elem))
-    v = torch.tensor([halo_t, feat_t, float(halo_f), float(halo_b)], dtype=torch.float64,
+    # feature slicing pipelines its switches over `chunks` row chunks: the
+    # exchange overlaps the gathers / dense of other chunks, one chunk's worth
+    # of it stays exposed (the halo path overlaps only halo-free rows: additive)
+    feat_comm = 4 * (world - 1) * (r1 - r0) * fc * elem / link
+    feat_comp = (2 * e * (fc * elem + 4) / _gather_rate(fc * elem) + dense_own
+                 + 5 * 2 * (r1 - r0) * row / _DENSE_BPS)         # + layout switches
+    feat_t = max(feat_comm, feat_comp) + feat_comm / _FEAT_CHUNKS
+    rep_t = (2 * e * (row + 4) / _gather_rate(row)
+             + _DENSE_BYTES_PER_ROW_FS * num_nodes * row / _DENSE_BPS)
+    v = torch.tensor([halo_t, feat_t, rep_t, float(halo_f), float(halo_b)], dtype=torch.float64,
                      device=edge_index.device)
     if world > 1:
         dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
-    halo_t, feat_t, hf, hb = v.tolist()
-    return {"halo_s": halo_t, "feature_s": feat_t, "halo_rows_fwd_max": int(hf),
-            "halo_rows_bwd_max": int(hb)}
+    halo_t, feat_t, rep_t, hf, hb = v.tolist()
+    return {"halo_s": halo_t, "feature_s": feat_t, "replicate_s": rep_t,
+            "halo_rows_fwd_max": int(hf), "halo_rows_bwd_max": int(hb)}
+
+
+@dataclass
+class ReplicaPartition:
+    """No sharding: every rank holds the whole graph and runs the whole block.
+    Chosen by the planner when any partition is modelled slower than one GPU
+    doing all the work (a random graph over a single xGMI link: W = 2)."""
+
+    rank: int
+    world: int
+    num_nodes: int
+    graph: SageGraph
+
+    row_begin = 0
+
+    @property
+    def row_end(self) -> int:
+        return self.num_nodes
+
+    @property
+    def num_rows(self) -> int:
+        return self.num_nodes
+
+    def exchange_bytes_per_layer(self, feat: int, elem: int) -> int:
+        return 0
+
+
+def partition_replicated(edge_index: torch.Tensor, num_nodes: int, world: int, rank: int,
+                         backend=HipBackend) -> ReplicaPartition:
+    if backend is HipBackend:
+        from .graph import build_graph
+        g = build_graph(edge_index, num_nodes)      # with the skew schedules (C5)
+    else:
+        rp, col, trp, tcol = backend.csr(edge_index, max(num_nodes, 1), True)
+        g = SageGraph(num_nodes, int(edge_index.size(1)), rp, col, trp, tcol)
+    return ReplicaPartition(rank, world, num_nodes, g)
 
 
 def plan_partition(edge_index: torch.Tensor, num_nodes: int, world: int, rank: int,
                    feat: int, elem: int, strategy: str = "auto", backend=HipBackend,
                    group=None, chunks: int = 4):
-    """Partition with ``strategy`` in {"auto", "halo", "feature"}; "auto" takes
-    the lower modelled time of :func:`estimate_strategies` (every rank gets the
-    same answer: the estimate is max-reduced).  Returns (partition, info)."""
+    """Partition with ``strategy`` in {"auto", "halo", "feature", "replicate"};
+    "auto" takes the lowest modelled time of :func:`estimate_strategies`
+    (every rank gets the same answer: the estimate is max-reduced).  Returns
+    (partition, info).  With "replicate" every rank runs the whole graph: the
+    caller passes all rows of x (``partition.row_begin/row_end`` span them)."""
     info = {}
     if strategy == "auto":
         if world == 1:
             strategy = "halo"
         else:
             info = estimate_strategies(edge_index, num_nodes, world, rank, feat, elem, group)
-            strategy = "feature" if info["feature_s"] < info["halo_s"] else "halo"
+            strategy = min(("halo", "feature", "replicate"), key=lambda k: info[f"{k}_s"])
     info["strategy"] = strategy
     if strategy == "feature":
         return partition_features(edge_index, num_nodes, world, rank, backend, chunks), info
+    if strategy == "replicate":
+        return partition_replicated(edge_index, num_nodes, world, rank, backend), info
     if strategy == "halo":
         return partition_graph(edge_index, num_nodes, world, rank, backend, group), info
-    raise ValueError(f"unknown partition strategy {strategy!r} (auto, halo, feature)")
+    raise ValueError(f"unknown partition strategy {strategy!r} "
+                     "(auto, halo, feature, replicate)")

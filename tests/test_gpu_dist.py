@@ -155,12 +155,14 @@ def _mp_worker(rank, world, port, strategy, dtype_name, q):
         out_b.backward(gout[r0:r1])
         torch.cuda.synchronize()
         assert torch.equal(out_b, out_a[r0:r1]), "forward rows differ"
-        if dtype == torch.float32 or info["strategy"] == "halo":
+        if dtype == torch.float32 or info["strategy"] in ("halo", "replicate"):
             assert torch.equal(xb.grad, xa.grad[r0:r1]), "input grad differs"
         else:
             _close_in_range(xb.grad, xa.grad[r0:r1])
         for k, p in blk.named_parameters():
-            if info["strategy"] == "halo":
+            if info["strategy"] == "replicate":
+                assert torch.equal(p.grad, ga[k]), k
+            elif info["strategy"] == "halo":
                 torch.testing.assert_close(p.grad, ga[k], atol=2e-4, rtol=2e-4)
             else:
                 _grad_close(p.grad, ga[k], dtype, k)
@@ -173,7 +175,7 @@ def _mp_worker(rank, world, port, strategy, dtype_name, q):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("strategy", ["halo", "feature"])
+@pytest.mark.parametrize("strategy", ["halo", "feature", "replicate"])
 @pytest.mark.parametrize("dtype_name", ["float32", "bfloat16"])
 def test_two_ranks_one_gpu(strategy, dtype_name):
     """W = 2 processes sharing cuda:0 over gloo: the multi-rank protocol with

@@ -701,3 +701,74 @@ def test_cols_pack_unpack_match_torch(dtype, n, nblk, cs):
     add = torch.randn(n, nblk * cs, generator=gen, device=DEV).to(dtype)
     ops.cols_unpack(packed, n, nblk, cs, out, addend=add)
     assert torch.equal(out, add + rows)
+
+
+# -------------------------------------------------- full-size property (C4) --
+def _khop_on_gpu(src, dst, targets, layers, n):
+    """oracle.sage_ref.khop_subgraph's construction with GPU set operations:
+    nodes at in-hop distance < L keep all their in-edges (original order),
+    targets first in the returned node list."""
+    hop = targets
+    inner = [targets]
+    for _ in range(layers - 1):
+        hop = torch.unique(src[torch.isin(dst, hop)])
+        inner.append(hop)
+    inner = torch.unique(torch.cat(inner))
+    emask = torch.isin(dst, inner)
+    s, d = src[emask], dst[emask]
+    rest = torch.unique(torch.cat([s, d]))
+    nodes = torch.cat([targets, rest[~torch.isin(rest, targets)]])
+    remap = torch.full((n,), -1, dtype=torch.int64, device=src.device)
+    remap[nodes] = torch.arange(nodes.numel(), device=src.device)
+    return nodes, torch.stack([remap[s], remap[d]])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_full_size_c4_khop_parity(dtype):
+    """BASELINE C4 (10M nodes / 100M edges, F = 256, 2 layers) on the GPU: the
+    target rows' outputs, the input gradient over their 2-hop cone and every
+    parameter gradient of a loss reading only the targets equal the CPU oracle
+    run on the targets' in-neighbourhood subgraph -- the size-independent
+    property pinned on CPU by
+    tests/test_oracle.py::test_khop_subgraph_reproduces_full_graph.
+    Tolerances as test_sageblock_fwd_bwd (bf16 in the kink-free regime)."""
+    from oracle.sage_ref import RefSageBlock, set_synthetic_params
+    from sldm_sage import SageBlock
+    n, e, hd = 10_000_000, 100_000_000, [256, 256, 256]
+    gen = torch.Generator(device=DEV).manual_seed(4)
+    src = torch.randint(0, n, (e,), generator=gen, device=DEV)
+    dst = torch.randint(0, n, (e,), generator=gen, device=DEV)
+    x = torch.randn(n, hd[0], generator=gen, device=DEV).to(dtype)
+    ref = RefSageBlock(hd, None, 0.1)
+    set_synthetic_params(ref, seed=1)
+    if dtype == torch.bfloat16:
+        with torch.no_grad():
+            for post in ref.posts:
+                post[0].bias.fill_(4.0)
+    blk = SageBlock(hd, None, 0.1)
+    blk.load_state_dict(ref.state_dict())
+    blk = blk.to(DEV)
+    targets = torch.unique(torch.randint(0, n, (16,), generator=gen, device=DEV))
+    gout = torch.zeros(n, hd[-1], device=DEV, dtype=dtype)
+    gout[targets] = torch.randn(targets.numel(), hd[-1], generator=gen, device=DEV).to(dtype)
+    xg = x.requires_grad_(True)
+    out = blk(xg, torch.stack([src, dst]))
+    out.backward(gout)
+    torch.cuda.synchronize()
+
+    nodes, sub = _khop_on_gpu(src, dst, targets, len(hd) - 1, n)
+    assert sub.numel() and int(sub.min()) >= 0
+    xs = x.detach()[nodes].float().cpu().requires_grad_(True)
+    out_s = ref(xs, sub.cpu())
+    out_s.backward(gout[nodes].float().cpu())
+    t = targets.numel()
+    refp = dict(ref.named_parameters())
+    pairs = [("out", out[targets], out_s[:t].detach()), ("dx", xg.grad[nodes], xs.grad)]
+    pairs += [(k, p.grad, refp[k].grad) for k, p in blk.named_parameters()]
+    tol = TOL[dtype]
+    for name, got, want in pairs:
+        scale = 1.0
+        if dtype == torch.bfloat16 or name not in ("out", "dx"):
+            scale = max(1.0, want.abs().max().item())
+        torch.testing.assert_close(got.float().cpu() / scale, want / scale, **tol,
+                                   msg=lambda m: f"{name}: {m}")
