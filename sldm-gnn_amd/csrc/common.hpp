@@ -220,6 +220,14 @@ int stream_dense_fwd(const void* a0, int64_t lda0, int64_t k0, const void* a1, i
 int stream_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int64_t ldb,
                          int64_t num_rows, int64_t nc, const int32_t* rowptr, int64_t scale_cols,
                          void* out, int64_t ldo, void* out2, int64_t ldo2, hipStream_t stream);
+// gemm_ws.hip: weight-stationary dX kernel (weights in VGPRs, LDS-DMA tiles).
+bool ws_gemm_enabled();
+bool ws_rowscale_ok(int64_t k, int64_t nc, int64_t num_rows, const void* a, int64_t lda,
+                    const void* b, int64_t ldb, const void* out, int64_t ldo, const void* out2,
+                    int64_t ldo2, int64_t scale_cols);
+int ws_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int64_t ldb,
+                     int64_t num_rows, int64_t nc, const int32_t* rowptr, int64_t scale_cols,
+                     void* out, int64_t ldo, void* out2, int64_t ldo2, hipStream_t stream);
 
 }  // namespace sldm
 

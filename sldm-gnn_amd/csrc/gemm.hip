@@ -720,6 +720,11 @@ extern "C" int sldm_gemm_nt_rowscale(int dtype, const void* a, int64_t lda, int6
   if (num_rows == 0) return SLDM_OK;
   SLDM_REQUIRE(a && b && out, "sldm_gemm_nt_rowscale: NULL argument");
   hipStream_t stream = sldm::as_stream(stream_);
+  if (dtype == SLDM_BF16 && sldm::ws_gemm_enabled() &&
+      sldm::ws_rowscale_ok(k, nc, num_rows, a, lda, b, ldb, out, ldo, out2, ldo2,
+                           rowptr || out2 ? scale_cols : 0))
+    return sldm::ws_gemm_rowscale(a, lda, k, b, ldb, num_rows, nc, rowptr, scale_cols, out, ldo,
+                                  out2, ldo2, stream);
   if (dtype == SLDM_BF16 && sldm::stream_gemm_enabled() &&
       sldm::stream_rowscale_ok(k, nc, a, lda, b, ldb, out, ldo, scale_cols) &&
       (!out2 || (ldo2 == ldo && scale_cols % 256 == 0 &&

@@ -593,6 +593,38 @@ def test_stream_gemm_rowscale_vs_torch(m, fi):
     torch.testing.assert_close(torch.cat([lo, hi], 1).float(), ref, atol=3e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("m", STREAM_ROWS + [63, 65, 130_000])
+@pytest.mark.parametrize("fi", [128, 256])
+def test_ws_gemm_rowscale_bit_exact_vs_stream(m, fi, monkeypatch):
+    """gemm_ws.hip (weights in VGPRs, LDS-DMA activation tiles) runs the stream
+    kernel's MFMA sequence: every output bit equal, with and without the 1/deg
+    scale, split and one-buffer outputs, ragged final tiles (m % 64 != 0)."""
+    from sldm_sage import build_graph, ops
+    from oracle.sage_ref import random_graph
+    fo = 256
+    ei, _ = random_graph(m, 3 * m + 1, 1, seed=m + 7)
+    g = build_graph(ei.to(DEV), m)
+    gen = torch.Generator(device=DEV).manual_seed(m + 3 * fi)
+    dh = torch.randn(m, fo, generator=gen, device=DEV).bfloat16()
+    wt = (torch.randn(2 * fi, fo, generator=gen, device=DEV) / 16).bfloat16()
+
+    def run(ws, rowptr, split):
+        monkeypatch.setenv("SLDM_WS_GEMM", "1" if ws else "0")
+        r = ops.gemm_nt_rowscale(dh, wt, rowptr, fi, split=split)
+        torch.cuda.synchronize()
+        return torch.cat(r, 1) if split else r
+
+    for rowptr in (g.rowptr, None):
+        got = run(True, rowptr, False)
+        assert torch.equal(got, run(False, rowptr, False))
+        ref = dh.float() @ wt.float().t()
+        if rowptr is not None:
+            ref[:, :fi] /= (rowptr[1:] - rowptr[:-1]).clamp(min=1).float()[:, None]
+        torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
+        split = run(True, rowptr, True)
+        assert torch.equal(split, got)
+
+
 # ------------------------------------------------ overlapped (split) gather --
 @pytest.mark.parametrize("mean", [True, False])
 def test_overlapped_gather_split_is_bit_exact(mean):

@@ -85,6 +85,11 @@ def main():
         add("gemm_nt_rowscale N=2f split", timeit(
             lambda: ops.gemm_nt_rowscale(dh, wt, gr.rowptr, f, split=True), a.reps),
             (n * f + n * 2 * f) * s, fl)
+        os.environ["SLDM_WS_GEMM"] = "0"
+        add("gemm_nt_rowscale N=2f split stream", timeit(
+            lambda: ops.gemm_nt_rowscale(dh, wt, gr.rowptr, f, split=True), a.reps),
+            (n * f + n * 2 * f) * s, fl)
+        os.environ.pop("SLDM_WS_GEMM")
         add("gemm_nt_rowscale N=f", timeit(lambda: ops.gemm_nt_rowscale(dh, wcat[:, :f].contiguous(),
                                                                          None, 0), a.reps),
             (n * f + n * f) * s, fl / 2)
