@@ -222,12 +222,28 @@ int stream_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, i
                          void* out, int64_t ldo, void* out2, int64_t ldo2, hipStream_t stream);
 // gemm_ws.hip: weight-stationary dX kernel (weights in VGPRs, LDS-DMA tiles).
 bool ws_gemm_enabled();
+bool ws_fwd_enabled();
+// gemm_tn_dma.hip: row-streaming dW kernel (LDS-DMA, transposed reads).
+bool tn_dma_enabled();
+bool tn_dma_ok(int64_t mo, int64_t n0, int64_t n1, int64_t rows, const void* a, int64_t lda,
+               const void* b0, int64_t ldb0, const void* b1, int64_t ldb1);
+size_t tn_dma_workspace_bytes(int64_t rows, int64_t nn);
+int tn_dma(const void* a, int64_t lda, const void* b0, int64_t ldb0, const void* b1, int64_t ldb1,
+           int64_t n1, int64_t rows, float* slab, int* splits_out, hipStream_t stream);
 bool ws_rowscale_ok(int64_t k, int64_t nc, int64_t num_rows, const void* a, int64_t lda,
                     const void* b, int64_t ldb, const void* out, int64_t ldo, const void* out2,
                     int64_t ldo2, int64_t scale_cols);
 int ws_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int64_t ldb,
                      int64_t num_rows, int64_t nc, const int32_t* rowptr, int64_t scale_cols,
                      void* out, int64_t ldo, void* out2, int64_t ldo2, hipStream_t stream);
+bool ws_dense_fwd_ok(int64_t k0, int64_t k1, int64_t nc, int64_t num_rows, const void* a0,
+                     int64_t lda0, const void* a1, int64_t lda1, const void* w, const void* out,
+                     const void* xhat);
+int ws_dense_fwd(const void* a0, int64_t lda0, int64_t k0, const void* a1, int64_t lda1,
+                 int64_t k1, const void* w, int64_t num_rows, const float* bias,
+                 const float* gamma, const float* beta, float eps, float slope, float drop_p,
+                 uint64_t seed, int64_t row_off, void* out, void* xhat, float* rstd,
+                 hipStream_t stream);
 
 }  // namespace sldm
 

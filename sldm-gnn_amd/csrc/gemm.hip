@@ -671,6 +671,10 @@ extern "C" int sldm_sage_dense_fwd(int dtype, const void* a0, int64_t lda0, int6
   SLDM_REQUIRE(a0 && w && out && gamma && beta && (k1 == 0 || a1),
                "sldm_sage_dense_fwd: NULL argument");
   hipStream_t stream = sldm::as_stream(stream_);
+  if (dtype == SLDM_BF16 && sldm::ws_fwd_enabled() &&
+      sldm::ws_dense_fwd_ok(k0, k1, nc, num_rows, a0, lda0, a1, lda1, w, out, xhat))
+    return sldm::ws_dense_fwd(a0, lda0, k0, a1, lda1, k1, w, num_rows, bias, gamma, beta, eps,
+                              negative_slope, drop_p, seed, row_off, out, xhat, rstd, stream);
   if (dtype == SLDM_BF16 && sldm::stream_gemm_enabled() &&
       sldm::stream_dense_fwd_ok(k0, k0 + k1, nc, a0, lda0, k1 ? a1 : a0, k1 ? lda1 : lda0, w,
                                 out, xhat))
@@ -757,7 +761,10 @@ extern "C" int sldm_gemm_nt_rowscale(int dtype, const void* a, int64_t lda, int6
 extern "C" size_t sldm_gemm_tn_workspace_bytes(int64_t num_rows, int64_t mo, int64_t nn) {
   if (num_rows <= 0 || mo <= 0 || nn <= 0) return 16;
   TnPlan pl = tn_plan(num_rows, mo, nn);
-  return sizeof(float) * (size_t)pl.splits * (size_t)mo * (size_t)nn + 256;
+  size_t need = sizeof(float) * (size_t)pl.splits * (size_t)mo * (size_t)nn + 256;
+  if (mo == 256 && (nn == 256 || nn == 512))   // gemm_tn_dma.hip's slab may be larger
+    need = std::max(need, sldm::tn_dma_workspace_bytes(num_rows, nn));
+  return need;
 }
 
 extern "C" int sldm_gemm_tn(int dtype, const void* a, int64_t lda, int64_t mo, const void* b0,
@@ -777,8 +784,19 @@ extern "C" int sldm_gemm_tn(int dtype, const void* a, int64_t lda, int64_t mo, c
   const size_t need = sldm_gemm_tn_workspace_bytes(num_rows, mo, nn);
   SLDM_REQUIRE(workspace && ws_bytes >= need, "sldm_gemm_tn: workspace too small (%zu < %zu)",
                ws_bytes, need);
-  TnPlan pl = tn_plan(num_rows, mo, nn);
   float* slab = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(workspace) + 255) & ~(uintptr_t)255);
+  if (dtype == SLDM_BF16 && sldm::tn_dma_enabled() &&
+      sldm::tn_dma_ok(mo, n0, n1, num_rows, a, lda, b0, ldb0, b1, ldb1)) {
+    int splits = 0;
+    const int rc = sldm::tn_dma(a, lda, b0, ldb0, b1, ldb1, n1, num_rows, slab, &splits, stream);
+    if (rc != SLDM_OK) return rc;
+    const int64_t n = mo * nn;
+    slab_reduce_kernel<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, stream>>>(
+        slab, splits, n, out);
+    SLDM_LAUNCH_CHECK("slab_reduce_kernel");
+    return SLDM_OK;
+  }
+  TnPlan pl = tn_plan(num_rows, mo, nn);
   auto run = [&](auto* tag) -> int {
     using T = std::remove_pointer_t<decltype(tag)>;
     constexpr int EPV = 16 / sizeof(T);

@@ -229,6 +229,264 @@ __global__ __launch_bounds__(kThreads) void ws_rowscale_kernel(WsArgs p) {
   wait_vm<0>();   // retire the tail's dummy DMAs before the workgroup ends
 }
 
+// ---------------------------------------------------------------------------
+// Forward dense layer, same weight-stationary scheme, LayerNorm epilogue:
+//   z = [a0 | a1] @ W^T + bias  (W [256][K], K = k0 + k1),
+//   xhat = (z - mean) * rstd, out = dropout(act(xhat * gamma + beta)).
+// Wave w holds output columns [32w, 32w + 32) (CT = 2 tiles) x all K of W
+// (KSTEPS*8 VGPRs: 128 at K = 512).  A tile slot holds two LDS sub-tiles,
+// [TM][k0] from a0 then [TM][k1] from a1, each row-XOR-swizzled; every DMA
+// instruction lands in one sub-tile, so its 64 lanes share one SGPR base.
+// Each row's 256 columns are spread over the 8 waves, so the LayerNorm
+// statistics reduce in two steps: the wave's 32 columns in registers (lanes
+// q = 0..3 by swizzle / shuffle), then the 8 wave partials merged through LDS
+// (epilogue comment).
+struct WsLnArgs {
+  const uint16_t* a0; int64_t lda0;
+  const uint16_t* a1; int64_t lda1;
+  const uint16_t* w;                  // [256][K]
+  int64_t M; int64_t ntiles;
+  uint16_t* out; uint16_t* xhat; float* rstd;   // [M][256], [M][256], [M]
+  const float* bias; const float* gamma; const float* beta;
+  float eps, slope, drop_p, drop_scale; uint64_t seed; int64_t row_off;
+};
+
+template <int KSTEPS, int NBUF, int TM>
+constexpr size_t ws_ln_lds_bytes() {
+  return (size_t)NBUF * TM * KSTEPS * 64 + 3 * 256 * sizeof(float) + TM * 8 * sizeof(float2);
+}
+
+template <int KSTEPS, int K0STEPS, int NBUF, int TM>
+__global__ __launch_bounds__(kThreads) void ws_ln_kernel(WsLnArgs p) {
+  constexpr int CT = 2;
+  constexpr int K1STEPS = KSTEPS - K0STEPS;
+  constexpr int RB0 = K0STEPS * 64, RB1 = K1STEPS * 64;   // sub-tile row bytes
+  constexpr int TB = TM * KSTEPS * 64;                    // tile bytes (16 or 32 KB)
+  constexpr int RG = TM / 16;
+  constexpr int DPW = TB / 1024 / 8;
+  constexpr int SUB1 = TM * RB0;                          // byte offset of sub-tile 1
+  constexpr int OPS_DMA = DPW;
+  static_assert(K0STEPS % 4 == 0 && K1STEPS % 4 == 0 && SUB1 % 1024 == 0, "sub-tile shape");
+  static_assert(TB % 8192 == 0 && NBUF >= 2, "tile shape");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* prm = reinterpret_cast<float*>(smem + NBUF * TB);   // bias | gamma | beta
+  float2* red = reinterpret_cast<float2*>(prm + 3 * 256);     // [TM][8] (mean_w, M2_w)
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  if ((int64_t)blockIdx.x >= p.ntiles) return;
+  const int64_t grid = gridDim.x;
+
+  for (int c = tid; c < 256; c += kThreads) {
+    prm[c] = p.bias ? p.bias[c] : 0.f;
+    prm[256 + c] = p.gamma[c];
+    prm[512 + c] = p.beta[c];
+  }
+
+  const int cbase = wave * 16 * CT;
+  const int64_t K = KSTEPS * 32;
+  s8v wf[CT][KSTEPS];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s)
+      wf[ct][s] = *reinterpret_cast<const s8v*>(
+          p.w + (int64_t)(cbase + 16 * ct + (lane & 15)) * K + 32 * s + 8 * (lane >> 4));
+
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_vptr)smem;
+  auto tile_of = [&](int64_t n) -> int64_t {
+    const int64_t t = blockIdx.x + n * grid;
+    return t < p.ntiles ? t : (int64_t)blockIdx.x;
+  };
+  auto issue = [&](int64_t n) {
+    const int64_t r0 = tile_of(n) * TM;
+    const int64_t last = p.M - 1 - r0;
+    int ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+#pragma unroll
+    for (int j = 0; j < DPW; ++j) {
+      const int d = wave * DPW + j;                 // wave-uniform
+      const bool sub1 = d * 1024 >= SUB1;
+      const int ob = sub1 ? d * 1024 - SUB1 : d * 1024;
+      const int gsub = (sub1 ? RB1 : RB0) / 16;     // granules per sub-tile row
+      const int gp = ob / 16 + ln;
+      const int r = gp / gsub, jg = gp % gsub;
+      const int64_t rr = r < last ? r : last;
+      const char* base = reinterpret_cast<const char*>(sub1 ? p.a1 + r0 * p.lda1
+                                                            : p.a0 + r0 * p.lda0);
+      const int64_t lda = sub1 ? p.lda1 : p.lda0;
+      uint32_t la = lds0 + (uint32_t)((n % NBUF) * TB + d * 1024);
+      asm volatile("" : "+s"(base), "+s"(la));
+      dma16(base, (uint32_t)(rr * lda * 2 + 16 * (jg ^ (r & 15))), la);
+    }
+  };
+
+#pragma unroll
+  for (int n = 0; n < NBUF - 1; ++n) issue(n);
+
+  const float inv_n = 1.0f / 256.f;
+  const uint32_t dthr = sldm::dropout_threshold(p.drop_p);
+  const bool hasx = p.xhat != nullptr;
+
+  for (int64_t n = 0;; ++n) {
+    const int64_t tile = blockIdx.x + n * grid;
+    if (tile >= p.ntiles) break;
+    int i, q;
+    {
+      int ln;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+      i = ln & 15;
+      q = ln >> 4;
+    }
+    // stores per wave per tile: RG out (+ RG xhat); wave 0's extra rstd
+    // stores only make its count stricter
+    constexpr int SPO = RG;
+    if (n < NBUF - 1) {
+      wait_vm<(NBUF - 2) * OPS_DMA>();
+    } else if (hasx) {
+      wait_vm<2 * SPO + (NBUF - 2) * (OPS_DMA + 2 * SPO)>();
+    } else {
+      wait_vm<SPO + (NBUF - 2) * (OPS_DMA + SPO)>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(n + NBUF - 1);
+
+    const char* slot = smem + (n % NBUF) * TB;
+    f4v acc[RG][CT];
+#pragma unroll
+    for (int m = 0; m < RG; ++m)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[m][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+    s8v bf[2][RG];
+    auto read_b = [&](int s, s8v (&dst)[RG]) {
+      const bool s1 = s >= K0STEPS;
+      const int ls = s1 ? s - K0STEPS : s;
+      const char* sb = slot + (s1 ? SUB1 : 0);
+      const int rb = s1 ? RB1 : RB0;
+      const int goff = 16 * ((4 * ls + q) ^ i);
+#pragma unroll
+      for (int m = 0; m < RG; ++m)
+        dst[m] = *reinterpret_cast<const s8v*>(sb + (16 * m + i) * rb + goff);
+    };
+    read_b(0, bf[0]);
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+      if (s + 1 < KSTEPS) read_b(s + 1, bf[(s + 1) & 1]);
+#pragma unroll
+      for (int m = 0; m < RG; ++m)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+          acc[m][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ct][s], bf[s & 1][m], acc[m][ct],
+                                                              0, 0, 0);
+      if (s + 1 < KSTEPS) __builtin_amdgcn_sched_group_barrier(0x100, RG, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, RG * CT, 0);
+    }
+
+    // ---- LayerNorm epilogue: acc[m][ct][r] = z[row 16m+i][col cbase+16ct+4q+r]
+    // Statistics by Chan's pairwise merge: each wave reduces its 32 columns
+    // to (mean_w, M2_w) (two passes in registers), one LDS exchange, then
+    //   mean = sum_w mean_w / 8,  M2 = sum_w M2_w + 32 sum_w (mean_w - mean)^2
+    // summed in wave order (identical in every wave): one barrier per tile.
+    const int cq = cbase + 4 * q;
+#pragma unroll
+    for (int m = 0; m < RG; ++m) {
+      float sm = 0.f;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const f4v bb = *reinterpret_cast<const f4v*>(prm + cq + 16 * ct);
+        acc[m][ct] += bb;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm += acc[m][ct][r];
+      }
+      sm += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(sm), 0x401F));
+      sm += __shfl_xor(sm, 32, 64);
+      const float mw = sm * (1.0f / 32.f);
+      float m2 = 0.f;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = acc[m][ct][r] - mw;
+          m2 += d * d;
+        }
+      m2 += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(m2), 0x401F));
+      m2 += __shfl_xor(m2, 32, 64);
+      if (q == 0) red[(16 * m + i) * 8 + wave] = make_float2(mw, m2);
+    }
+    __syncthreads();
+    const int64_t r0 = tile * TM;
+    const int ccol = cbase + ((q & 1) ? 16 + 4 * (q - 1) : 4 * q);
+#pragma unroll
+    for (int m = 0; m < RG; ++m) {
+      const float2* rr = red + (16 * m + i) * 8;
+      float2 st[8];
+#pragma unroll
+      for (int w = 0; w < 8; ++w) st[w] = rr[w];
+      float msum = st[0].x;
+#pragma unroll
+      for (int w = 1; w < 8; ++w) msum += st[w].x;
+      const float mean = msum * (1.0f / 8.f);
+      float m2 = st[0].y, dm = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        if (w) m2 += st[w].y;
+        const float d = st[w].x - mean;
+        dm += d * d;
+      }
+      const float var = (m2 + 32.f * dm) * inv_n;
+      const float rs = 1.0f / sqrtf(var + p.eps);
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[m][ct][r] = (acc[m][ct][r] - mean) * rs;
+      // rows past M recompute row M-1 (clamped loads): clamp the row (dropout
+      // key included) so their stores rewrite row M-1's own values
+      const int64_t row = r0 + 16 * m + i < p.M ? r0 + 16 * m + i : p.M - 1;
+      if (p.rstd && wave == 0 && q == 0) p.rstd[row] = rs;
+      if (hasx) {
+        uint32_t w2[2][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          w2[h][0] = sldm::pack_bf16x2(acc[m][h][0], acc[m][h][1]);
+          w2[h][1] = sldm::pack_bf16x2(acc[m][h][2], acc[m][h][3]);
+        }
+        auto s0 = __builtin_amdgcn_permlane16_swap(w2[0][0], w2[1][0], false, false);
+        auto s1 = __builtin_amdgcn_permlane16_swap(w2[0][1], w2[1][1], false, false);
+        *reinterpret_cast<uint4*>(p.xhat + row * 256 + ccol) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      }
+      const uint32_t rkey = sldm::dropout_row_key(p.seed, (uint64_t)(row + p.row_off));
+      uint32_t w2[2][2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = cq + 16 * h;
+        const f4v gg = *reinterpret_cast<const f4v*>(prm + 256 + c);
+        const f4v be = *reinterpret_cast<const f4v*>(prm + 512 + c);
+        bool keep[4] = {true, true, true, true};
+        if (p.drop_p > 0.f) {
+          sldm::dropout_keep2(rkey, (uint32_t)c, dthr, keep[0], keep[1]);
+          sldm::dropout_keep2(rkey, (uint32_t)c + 2, dthr, keep[2], keep[3]);
+        }
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float y = acc[m][h][r] * gg[r] + be[r];
+          const float a = y > 0.f ? y : y * p.slope;
+          v[r] = keep[r] ? a * p.drop_scale : 0.f;
+        }
+        w2[h][0] = sldm::pack_bf16x2(v[0], v[1]);
+        w2[h][1] = sldm::pack_bf16x2(v[2], v[3]);
+      }
+      auto s0 = __builtin_amdgcn_permlane16_swap(w2[0][0], w2[1][0], false, false);
+      auto s1 = __builtin_amdgcn_permlane16_swap(w2[0][1], w2[1][1], false, false);
+      *reinterpret_cast<uint4*>(p.out + row * 256 + ccol) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+    }
+  }
+  wait_vm<0>();
+}
+
 int g_num_cus = 0;
 int num_cus() {
   if (g_num_cus == 0) {
@@ -257,6 +515,20 @@ int launch_ws(WsArgs& p, hipStream_t stream) {
   return SLDM_OK;
 }
 
+template <int KSTEPS, int K0STEPS, int NBUF, int TM>
+int launch_ws_ln(WsLnArgs& p, hipStream_t stream) {
+  constexpr size_t lds = ws_ln_lds_bytes<KSTEPS, NBUF, TM>();
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  p.ntiles = (p.M + TM - 1) / TM;
+  const int64_t grid = std::min<int64_t>(p.ntiles, num_cus());
+  auto kern = ws_ln_kernel<KSTEPS, K0STEPS, NBUF, TM>;
+  SLDM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  kern<<<(unsigned)grid, kThreads, lds, stream>>>(p);
+  SLDM_LAUNCH_CHECK("ws_ln_kernel");
+  return SLDM_OK;
+}
+
 bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
 
 }  // namespace
@@ -267,6 +539,15 @@ namespace sldm {
 bool ws_gemm_enabled() {
   const char* e = getenv("SLDM_WS_GEMM");
   return !(e && e[0] == '0');
+}
+// The weight-stationary forward is opt-in (SLDM_WS_FWD=1): with each row's
+// 256 columns spread over 8 waves its per-row epilogue work (statistics merge,
+// dropout row key, addressing) is repeated by 32 lanes instead of 4, ~55 VALU
+// instructions per output element against the stream kernel's ~15, and it
+// measured 5.4-5.6 ms against 4.8 at C4.
+bool ws_fwd_enabled() {
+  const char* e = getenv("SLDM_WS_FWD");
+  return ws_gemm_enabled() && e && e[0] == '1';
 }
 
 // Shape gate: bf16 (caller), K = 256, Nc = 512 (CT = 4) or 256 (CT = 2),
@@ -296,6 +577,54 @@ int ws_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int64
   if (nc == 512)
     return rowptr ? launch_ws<8, 4, 4, true>(p, stream) : launch_ws<8, 4, 4, false>(p, stream);
   return rowptr ? launch_ws<8, 2, 4, true>(p, stream) : launch_ws<8, 2, 4, false>(p, stream);
+}
+
+// Shape gate: bf16 (caller), 256 output columns, K = k0 + k1 of 256 or 512
+// split on a 128-column boundary, contiguous [M][256] outputs, 16-B aligned
+// rows and bases, 32-bit DMA offsets.
+bool ws_dense_fwd_ok(int64_t k0, int64_t k1, int64_t nc, int64_t num_rows, const void* a0,
+                     int64_t lda0, const void* a1, int64_t lda1, const void* w, const void* out,
+                     const void* xhat) {
+  const int64_t K = k0 + k1;
+  if (nc != 256 || (K != 256 && K != 512) || k0 % 128 || k1 % 128) return false;
+  if (num_rows >= (int64_t(1) << 30) || lda0 % 8 || lda0 > (1 << 20)) return false;
+  if (k1 && (lda1 % 8 || lda1 > (1 << 20) || !aligned16(a1))) return false;
+  return aligned16(a0) && aligned16(w) && aligned16(out) && (!xhat || aligned16(xhat));
+}
+
+int ws_dense_fwd(const void* a0, int64_t lda0, int64_t k0, const void* a1, int64_t lda1,
+                 int64_t k1, const void* w, int64_t num_rows, const float* bias,
+                 const float* gamma, const float* beta, float eps, float slope, float drop_p,
+                 uint64_t seed, int64_t row_off, void* out, void* xhat, float* rstd,
+                 hipStream_t stream) {
+  WsLnArgs p{};
+  p.a0 = (const uint16_t*)a0; p.lda0 = lda0;
+  p.a1 = k1 ? (const uint16_t*)a1 : (const uint16_t*)a0; p.lda1 = k1 ? lda1 : lda0;
+  p.w = (const uint16_t*)w;
+  p.M = num_rows;
+  p.out = (uint16_t*)out; p.xhat = (uint16_t*)xhat; p.rstd = rstd;
+  p.bias = bias; p.gamma = gamma; p.beta = beta; p.eps = eps; p.slope = slope;
+  p.drop_p = drop_p;
+  p.drop_scale = drop_p >= 1.f ? 0.f : (drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f);
+  p.seed = seed; p.row_off = row_off;
+  const int64_t K = k0 + k1;
+  // SLDM_WS_LN_ROWS=64: 64-row tiles (2-slot ring) instead of 32 (4 slots)
+  const char* e = getenv("SLDM_WS_LN_ROWS");
+  const bool big = e && atoi(e) == 64;
+  if (K == 512) {
+    if (big) {
+      if (k0 == 256) return launch_ws_ln<16, 8, 2, 64>(p, stream);
+      if (k0 == 128) return launch_ws_ln<16, 4, 2, 64>(p, stream);
+      if (k0 == 384) return launch_ws_ln<16, 12, 2, 64>(p, stream);
+      return launch_ws_ln<16, 16, 2, 64>(p, stream);
+    }
+    if (k0 == 256) return launch_ws_ln<16, 8, 4, 32>(p, stream);
+    if (k0 == 128) return launch_ws_ln<16, 4, 4, 32>(p, stream);
+    if (k0 == 384) return launch_ws_ln<16, 12, 4, 32>(p, stream);
+    return launch_ws_ln<16, 16, 4, 32>(p, stream);
+  }
+  if (k0 == 128) return launch_ws_ln<8, 4, 4, 64>(p, stream);
+  return launch_ws_ln<8, 8, 4, 64>(p, stream);
 }
 
 }  // namespace sldm

@@ -537,9 +537,13 @@ def test_gemm_tn_large_split(dtype):
 STREAM_ROWS = [1, 255, 256, 257, 2000, 70_001]
 
 
-@pytest.mark.parametrize("m", STREAM_ROWS)
+@pytest.mark.parametrize("m", STREAM_ROWS + [63, 65])
 @pytest.mark.parametrize("fi", [128, 256])
-def test_stream_dense_fwd_vs_torch_and_mask(m, fi):
+@pytest.mark.parametrize("kernel", ["ws", "stream"])
+def test_stream_dense_fwd_vs_torch_and_mask(m, fi, kernel, monkeypatch):
+    """Both bf16 forward kernels: gemm_ws.hip (weights in VGPRs, LayerNorm
+    statistics reduced across the 8 waves through LDS) and gemm_stream.hip."""
+    monkeypatch.setenv("SLDM_WS_FWD", "1" if kernel == "ws" else "0")
     from sldm_sage import ops
     from sldm_sage.dense import weight_cat
     fo, p, seed = 256, 0.25, 4242
@@ -565,6 +569,66 @@ def test_stream_dense_fwd_vs_torch_and_mask(m, fi):
     torch.testing.assert_close(out.float()[kept], z[kept], atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(xhat.float(), xh, atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(rstd, rs.squeeze(1), atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("rows", [1, 31, 32, 33, 1000, 70_001, 2_000_003])
+@pytest.mark.parametrize("n1", [0, 256])
+def test_tn_dma_weight_grad_vs_torch(rows, n1, monkeypatch):
+    """gemm_tn_dma.hip (row-streaming dW, LDS-DMA + transposed LDS reads,
+    partial last k-step masked) against an fp32 torch reference and against
+    gemm.hip's tile kernel (different split boundaries: equal within fp32
+    summation-order rounding)."""
+    from sldm_sage import ops
+    gen = torch.Generator(device=DEV).manual_seed(rows + n1)
+    dz = torch.randn(rows, 256, generator=gen, device=DEV).bfloat16()
+    b0 = torch.randn(rows, 256, generator=gen, device=DEV).bfloat16()
+    b1 = torch.randn(rows, 256, generator=gen, device=DEV).bfloat16() if n1 else None
+
+    def run(dma):
+        monkeypatch.setenv("SLDM_TN_DMA", "1" if dma else "0")
+        r = ops.gemm_tn(dz, b0, b1)
+        torch.cuda.synchronize()
+        return r
+
+    got, old = run(True), run(False)
+    ref = dz.double().t() @ (torch.cat([b0, b1], 1) if n1 else b0).double()
+    scale = max(1.0, float(rows) ** 0.5)
+    torch.testing.assert_close(got.double() / scale, ref / scale, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(got / scale, old / scale, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("m", [1, 65, 4097, 130_000])
+@pytest.mark.parametrize("k0,k1", [(256, 256), (128, 128), (256, 0), (512, 0), (128, 384)])
+def test_ws_dense_fwd_matches_stream(m, k0, k1, monkeypatch):
+    """The opt-in weight-stationary forward (SLDM_WS_FWD=1) and the default
+    kernel differ only in the LayerNorm statistics' fp32 summation order:
+    same dropout mask, outputs within one bf16 rounding."""
+    from sldm_sage import ops
+    gen = torch.Generator(device=DEV).manual_seed(m + k0)
+    a0 = torch.randn(m, k0, generator=gen, device=DEV).bfloat16()
+    a1 = torch.randn(m, max(k1, 8), generator=gen, device=DEV).bfloat16()
+    w = (torch.randn(256, k0 + k1, generator=gen, device=DEV) / (k0 + k1) ** 0.5).bfloat16()
+    b, g = (torch.randn(256, generator=gen, device=DEV) for _ in range(2))
+    be = torch.full((256,), 5.0, device=DEV)
+
+    def run(ws):
+        monkeypatch.setenv("SLDM_WS_FWD", "1" if ws else "0")
+        out = torch.empty(m, 256, dtype=torch.bfloat16, device=DEV)
+        xh = torch.empty_like(out)
+        rs = torch.empty(m, device=DEV)
+        ops._lib.check(ops._lib.load().sldm_sage_dense_fwd(
+            ops.dtype_code(a0), a0.data_ptr(), a0.stride(0), k0, a1.data_ptr(), a1.stride(0), k1,
+            w.data_ptr(), m, 256, b.data_ptr(), g.data_ptr(), be.data_ptr(), 1e-5, 0.1, 0.3, 99, 0,
+            out.data_ptr(), xh.data_ptr(), rs.data_ptr(), ops._stream(torch.device(DEV))),
+            "sldm_sage_dense_fwd")
+        torch.cuda.synchronize()
+        return out, xh, rs
+
+    (o1, x1, r1), (o2, x2, r2) = run(True), run(False)
+    assert torch.equal(o1 != 0, o2 != 0)
+    torch.testing.assert_close(r1, r2, atol=0, rtol=1e-5)
+    torch.testing.assert_close(x1.float(), x2.float(), atol=1e-2, rtol=1e-2)
+    torch.testing.assert_close(o1.float(), o2.float(), atol=3e-2, rtol=1e-2)
 
 
 @pytest.mark.parametrize("m", STREAM_ROWS)

@@ -79,6 +79,14 @@ def main():
                                                    save), a.reps)
             add(f"dense_fwd p={p_} save={save}", ms, (2 * n * f + n * f * (2 if save else 1)) * s,
                 fl)
+        for var, env in [("ws", {"SLDM_WS_FWD": "1"}),
+                         ("ws 64-row", {"SLDM_WS_FWD": "1", "SLDM_WS_LN_ROWS": "64"})]:
+            os.environ.update(env)
+            ms = timeit(lambda: ops.sage_dense_fwd(agg, x, wcat, b, gam, bet, 1e-5, 0.1, 0.25, 7,
+                                                   True), a.reps)
+            add(f"dense_fwd p=0.25 save=True {var}", ms, 4 * n * f * s, fl)
+            for k in env:
+                os.environ.pop(k)
     if want("nt"):
         add("gemm_nt_rowscale N=2f", timeit(lambda: ops.gemm_nt_rowscale(dh, wt, gr.rowptr, f),
                                             a.reps), (n * f + n * 2 * f) * s, fl)
@@ -95,6 +103,9 @@ def main():
             (n * f + n * f) * s, fl / 2)
     if want("tn"):
         add("gemm_tn", timeit(lambda: ops.gemm_tn(dh, agg, x), a.reps), 3 * n * f * s, fl)
+        os.environ["SLDM_TN_DMA"] = "0"
+        add("gemm_tn tiles", timeit(lambda: ops.gemm_tn(dh, agg, x), a.reps), 3 * n * f * s, fl)
+        os.environ.pop("SLDM_TN_DMA")
     if want("post"):
         out, xh, rs = ops.post_fwd(dh, None, gam, bet, 1e-5, 0.1, 0.0, 0, dt, True)
         for p_, zo in [(0.0, None), (0.25, None), (0.25, out)]:
