@@ -66,9 +66,9 @@ def main() -> None:
     hit = load_pass(a.hit) if a.hit else {}
     kernels = {}
     for k in sorted(set(fetch) & set(write)):
-        if not (k.startswith("gather_rows") or k.startswith("gemm") or k.startswith("post")
-                or k.startswith("slab") or k.startswith("colsum") or "narrow" in k
-                or "rowptr" in k):
+        if not (k.startswith("gather") or k.startswith("gemm") or k.startswith("post")
+                or k.startswith("ws_") or k.startswith("slab") or k.startswith("colsum")
+                or "narrow" in k or "rowptr" in k):
             continue
         f0 = fetch[k][min(fetch[k])].get("FETCH_SIZE", 0.0)
         w0 = write[k][min(write[k])].get("WRITE_SIZE", 0.0)
