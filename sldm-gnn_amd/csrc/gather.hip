@@ -57,6 +57,15 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(
   const int beg = rowptr[row];
   const int end = rowptr[row + 1];
 
+  // The addend row (root-path gradient) is independent of the neighbour
+  // loads: issue it first so it is in flight with them instead of costing
+  // one more dependent memory round trip after the last batch.
+  float a[NCH][V];
+  if constexpr (ADD) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) sldm::Vec<TO, V>::load(addend + row * lda + f0[c], a[c]);
+  }
+
   auto batch = [&](int k, auto u_const) {
     constexpr int U = decltype(u_const)::value;
     int idx[U];
@@ -92,11 +101,9 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     if (!act[c]) continue;
-    if (ADD) {
-      float a[V];
-      sldm::Vec<TO, V>::load(addend + row * lda + f0[c], a);
+    if constexpr (ADD) {
 #pragma unroll
-      for (int v = 0; v < V; ++v) acc[c][v] = a[v] + acc[c][v];
+      for (int v = 0; v < V; ++v) acc[c][v] = a[c][v] + acc[c][v];
     }
     sldm::Vec<TO, V>::store(out + row * ldo + f0[c], acc[c]);
   }

@@ -88,10 +88,13 @@ __global__ __launch_bounds__(kBlock) void gather_post_bwd_kernel(
       end_n = t_rowptr[row_n + 1];
     }
 
-    // xhat / rstd of the row first: in flight beside the gather
-    float xh[NCH][V];
+    // xhat / rstd / addend of the row first: in flight beside the gather
+    float xh[NCH][V], ad[NCH][V];
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) sldm::Vec<T, V>::load(xhat + row * (int64_t)feat + f0[c], xh[c]);
+    for (int c = 0; c < NCH; ++c) {
+      sldm::Vec<T, V>::load(xhat + row * (int64_t)feat + f0[c], xh[c]);
+      sldm::Vec<T, V>::load(addend + row * lda + f0[c], ad[c]);
+    }
     const float rs = rstd[row];
 
     // ---- transpose gather of row `row` (gather.hip's batching, CSR order)
@@ -126,10 +129,8 @@ __global__ __launch_bounds__(kBlock) void gather_post_bwd_kernel(
     float go[NCH][V];
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      float a[V];
-      sldm::Vec<T, V>::load(addend + row * lda + f0[c], a);
 #pragma unroll
-      for (int v = 0; v < V; ++v) go[c][v] = sldm::stored_value<T>(a[v] + acc[c][v]);
+      for (int v = 0; v < V; ++v) go[c][v] = sldm::stored_value<T>(ad[c][v] + acc[c][v]);
     }
 
     // ---- post backward of the layer below on that row (post.hip's math)

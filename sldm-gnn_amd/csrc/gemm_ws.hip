@@ -237,9 +237,8 @@ __global__ __launch_bounds__(kThreads) void ws_rowscale_kernel(WsArgs p) {
 // (KSTEPS*8 VGPRs: 128 at K = 512).  A tile slot holds two LDS sub-tiles,
 // [TM][k0] from a0 then [TM][k1] from a1, each row-XOR-swizzled; every DMA
 // instruction lands in one sub-tile, so its 64 lanes share one SGPR base.
-// Each row's 256 columns are spread over the 8 waves, so the LayerNorm
-// statistics reduce in two steps: the wave's 32 columns in registers (lanes
-// q = 0..3 by swizzle / shuffle), then the 8 wave partials merged through LDS
+// The MFMA layout spreads each row's 256 columns over the 8 waves; the
+// epilogue re-distributes z through LDS so that one wave owns whole rows
 // (epilogue comment).
 struct WsLnArgs {
   const uint16_t* a0; int64_t lda0;
@@ -253,7 +252,7 @@ struct WsLnArgs {
 
 template <int KSTEPS, int NBUF, int TM>
 constexpr size_t ws_ln_lds_bytes() {
-  return (size_t)NBUF * TM * KSTEPS * 64 + 3 * 256 * sizeof(float) + TM * 8 * sizeof(float2);
+  return (size_t)NBUF * TM * KSTEPS * 64 + 3 * 256 * sizeof(float) + (size_t)TM * 1024;
 }
 
 template <int KSTEPS, int K0STEPS, int NBUF, int TM>
@@ -271,7 +270,7 @@ __global__ __launch_bounds__(kThreads) void ws_ln_kernel(WsLnArgs p) {
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* prm = reinterpret_cast<float*>(smem + NBUF * TB);   // bias | gamma | beta
-  float2* red = reinterpret_cast<float2*>(prm + 3 * 256);     // [TM][8] (mean_w, M2_w)
+  char* zs = reinterpret_cast<char*>(prm + 3 * 256);          // [TM][256] fp32 z, swizzled
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -329,6 +328,7 @@ __global__ __launch_bounds__(kThreads) void ws_ln_kernel(WsLnArgs p) {
   const float inv_n = 1.0f / 256.f;
   const uint32_t dthr = sldm::dropout_threshold(p.drop_p);
   const bool hasx = p.xhat != nullptr;
+  const int nst = 2 + (hasx ? 2 : 0) + (p.rstd ? 1 : 0);
 
   for (int64_t n = 0;; ++n) {
     const int64_t tile = blockIdx.x + n * grid;
@@ -340,15 +340,17 @@ __global__ __launch_bounds__(kThreads) void ws_ln_kernel(WsLnArgs p) {
       i = ln & 15;
       q = ln >> 4;
     }
-    // stores per wave per tile: RG out (+ RG xhat); wave 0's extra rstd
-    // stores only make its count stricter
-    constexpr int SPO = RG;
+    // stores per wave per tile: 2 out (+ 2 xhat) (+ 1 rstd), the same in
+    // every wave
     if (n < NBUF - 1) {
       wait_vm<(NBUF - 2) * OPS_DMA>();
-    } else if (hasx) {
-      wait_vm<2 * SPO + (NBUF - 2) * (OPS_DMA + 2 * SPO)>();
     } else {
-      wait_vm<SPO + (NBUF - 2) * (OPS_DMA + SPO)>();
+      switch (nst) {
+        case 2: wait_vm<2 + (NBUF - 2) * (OPS_DMA + 2)>(); break;
+        case 3: wait_vm<3 + (NBUF - 2) * (OPS_DMA + 3)>(); break;
+        case 4: wait_vm<4 + (NBUF - 2) * (OPS_DMA + 4)>(); break;
+        default: wait_vm<5 + (NBUF - 2) * (OPS_DMA + 5)>(); break;
+      }
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -385,103 +387,75 @@ __global__ __launch_bounds__(kThreads) void ws_ln_kernel(WsLnArgs p) {
       __builtin_amdgcn_sched_group_barrier(0x008, RG * CT, 0);
     }
 
-    // ---- LayerNorm epilogue: acc[m][ct][r] = z[row 16m+i][col cbase+16ct+4q+r]
-    // Statistics by Chan's pairwise merge: each wave reduces its 32 columns
-    // to (mean_w, M2_w) (two passes in registers), one LDS exchange, then
-    //   mean = sum_w mean_w / 8,  M2 = sum_w M2_w + 32 sum_w (mean_w - mean)^2
-    // summed in wave order (identical in every wave): one barrier per tile.
-    const int cq = cbase + 4 * q;
+    // ---- epilogue, row-owner form: the MFMA layout spreads a row over all 8
+    // waves, so z goes to LDS (fp32, 16-B granule g of row r at g ^ (r & 7):
+    // conflict-free for both the writes below and the reads after the
+    // barrier) and wave w then owns tile rows 4w .. 4w+3 whole -- lane
+    // (rr = lane >> 4, l = lane & 15) holds columns 8l + 128t + e (t < 2,
+    // e < 8) of row 4w + rr, LayerNorm statistics reduce over its 16 lanes
+    // (DPP), and each row leaves as 256-B contiguous 16-B-per-lane stores.
 #pragma unroll
-    for (int m = 0; m < RG; ++m) {
-      float sm = 0.f;
+    for (int m = 0; m < RG; ++m)
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
-        const f4v bb = *reinterpret_cast<const f4v*>(prm + cq + 16 * ct);
-        acc[m][ct] += bb;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sm += acc[m][ct][r];
+        const int row = 16 * m + i, g = (cbase + 16 * ct + 4 * q) >> 2;
+        *reinterpret_cast<f4v*>(zs + row * 1024 + 16 * (g ^ (row & 7))) = acc[m][ct];
       }
-      sm += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(sm), 0x401F));
-      sm += __shfl_xor(sm, 32, 64);
-      const float mw = sm * (1.0f / 32.f);
-      float m2 = 0.f;
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float d = acc[m][ct][r] - mw;
-          m2 += d * d;
-        }
-      m2 += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(m2), 0x401F));
-      m2 += __shfl_xor(m2, 32, 64);
-      if (q == 0) red[(16 * m + i) * 8 + wave] = make_float2(mw, m2);
-    }
     __syncthreads();
-    const int64_t r0 = tile * TM;
-    const int ccol = cbase + ((q & 1) ? 16 + 4 * (q - 1) : 4 * q);
+    {
+      const int rr = lane >> 4, l = lane & 15;
+      const int trow = 4 * wave + rr;
+      const int64_t r0 = tile * TM;
+      // rows past M hold row M-1's values (clamped loads) and rewrite row M-1
+      const int64_t row = r0 + trow < p.M ? r0 + trow : p.M - 1;
+      float v[2][8];
+      float sm = 0.f;
 #pragma unroll
-    for (int m = 0; m < RG; ++m) {
-      const float2* rr = red + (16 * m + i) * 8;
-      float2 st[8];
-#pragma unroll
-      for (int w = 0; w < 8; ++w) st[w] = rr[w];
-      float msum = st[0].x;
-#pragma unroll
-      for (int w = 1; w < 8; ++w) msum += st[w].x;
-      const float mean = msum * (1.0f / 8.f);
-      float m2 = st[0].y, dm = 0.f;
-#pragma unroll
-      for (int w = 0; w < 8; ++w) {
-        if (w) m2 += st[w].y;
-        const float d = st[w].x - mean;
-        dm += d * d;
-      }
-      const float var = (m2 + 32.f * dm) * inv_n;
-      const float rs = 1.0f / sqrtf(var + p.eps);
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[m][ct][r] = (acc[m][ct][r] - mean) * rs;
-      // rows past M recompute row M-1 (clamped loads): clamp the row (dropout
-      // key included) so their stores rewrite row M-1's own values
-      const int64_t row = r0 + 16 * m + i < p.M ? r0 + 16 * m + i : p.M - 1;
-      if (p.rstd && wave == 0 && q == 0) p.rstd[row] = rs;
-      if (hasx) {
-        uint32_t w2[2][2];
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          w2[h][0] = sldm::pack_bf16x2(acc[m][h][0], acc[m][h][1]);
-          w2[h][1] = sldm::pack_bf16x2(acc[m][h][2], acc[m][h][3]);
+          const int g = 2 * l + 32 * t + h;
+          const f4v z = *reinterpret_cast<const f4v*>(zs + trow * 1024 + 16 * (g ^ (trow & 7)));
+          const f4v bb = *reinterpret_cast<const f4v*>(prm + 4 * g);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[t][4 * h + e] = z[e] + bb[e];
+            sm += v[t][4 * h + e];
+          }
         }
-        auto s0 = __builtin_amdgcn_permlane16_swap(w2[0][0], w2[1][0], false, false);
-        auto s1 = __builtin_amdgcn_permlane16_swap(w2[0][1], w2[1][1], false, false);
-        *reinterpret_cast<uint4*>(p.xhat + row * 256 + ccol) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-      }
+      const float mean = sldm::group_sum(sm, 16) * inv_n;
+      float v2 = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[t][e] -= mean;
+          v2 += v[t][e] * v[t][e];
+        }
+      const float rs = 1.0f / sqrtf(sldm::group_sum(v2, 16) * inv_n + p.eps);
+      if (p.rstd && l == 0) p.rstd[row] = rs;
       const uint32_t rkey = sldm::dropout_row_key(p.seed, (uint64_t)(row + p.row_off));
-      uint32_t w2[2][2];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int c = cq + 16 * h;
-        const f4v gg = *reinterpret_cast<const f4v*>(prm + 256 + c);
-        const f4v be = *reinterpret_cast<const f4v*>(prm + 512 + c);
-        bool keep[4] = {true, true, true, true};
+      for (int t = 0; t < 2; ++t) {
+        const int c0 = 8 * l + 128 * t;
+        float xh[8], o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xh[e] = v[t][e] * rs;
+        if (hasx) sldm::Vec<uint16_t, 8>::store(p.xhat + row * 256 + c0, xh);
+        bool keep[8] = {true, true, true, true, true, true, true, true};
         if (p.drop_p > 0.f) {
-          sldm::dropout_keep2(rkey, (uint32_t)c, dthr, keep[0], keep[1]);
-          sldm::dropout_keep2(rkey, (uint32_t)c + 2, dthr, keep[2], keep[3]);
-        }
-        float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float y = acc[m][h][r] * gg[r] + be[r];
-          const float a = y > 0.f ? y : y * p.slope;
-          v[r] = keep[r] ? a * p.drop_scale : 0.f;
+          for (int e = 0; e < 8; e += 2)
+            sldm::dropout_keep2(rkey, (uint32_t)(c0 + e), dthr, keep[e], keep[e + 1]);
         }
-        w2[h][0] = sldm::pack_bf16x2(v[0], v[1]);
-        w2[h][1] = sldm::pack_bf16x2(v[2], v[3]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float y = xh[e] * prm[256 + c0 + e] + prm[512 + c0 + e];
+          const float a = y > 0.f ? y : y * p.slope;
+          o[e] = keep[e] ? a * p.drop_scale : 0.f;
+        }
+        sldm::Vec<uint16_t, 8>::store(p.out + row * 256 + c0, o);
       }
-      auto s0 = __builtin_amdgcn_permlane16_swap(w2[0][0], w2[1][0], false, false);
-      auto s1 = __builtin_amdgcn_permlane16_swap(w2[0][1], w2[1][1], false, false);
-      *reinterpret_cast<uint4*>(p.out + row * 256 + ccol) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
     }
   }
   wait_vm<0>();
@@ -608,23 +582,14 @@ int ws_dense_fwd(const void* a0, int64_t lda0, int64_t k0, const void* a1, int64
   p.drop_scale = drop_p >= 1.f ? 0.f : (drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f);
   p.seed = seed; p.row_off = row_off;
   const int64_t K = k0 + k1;
-  // SLDM_WS_LN_ROWS=64: 64-row tiles (2-slot ring) instead of 32 (4 slots)
-  const char* e = getenv("SLDM_WS_LN_ROWS");
-  const bool big = e && atoi(e) == 64;
   if (K == 512) {
-    if (big) {
-      if (k0 == 256) return launch_ws_ln<16, 8, 2, 64>(p, stream);
-      if (k0 == 128) return launch_ws_ln<16, 4, 2, 64>(p, stream);
-      if (k0 == 384) return launch_ws_ln<16, 12, 2, 64>(p, stream);
-      return launch_ws_ln<16, 16, 2, 64>(p, stream);
-    }
-    if (k0 == 256) return launch_ws_ln<16, 8, 4, 32>(p, stream);
-    if (k0 == 128) return launch_ws_ln<16, 4, 4, 32>(p, stream);
-    if (k0 == 384) return launch_ws_ln<16, 12, 4, 32>(p, stream);
-    return launch_ws_ln<16, 16, 4, 32>(p, stream);
+    if (k0 == 256) return launch_ws_ln<16, 8, 3, 32>(p, stream);
+    if (k0 == 128) return launch_ws_ln<16, 4, 3, 32>(p, stream);
+    if (k0 == 384) return launch_ws_ln<16, 12, 3, 32>(p, stream);
+    return launch_ws_ln<16, 16, 3, 32>(p, stream);
   }
-  if (k0 == 128) return launch_ws_ln<8, 4, 4, 64>(p, stream);
-  return launch_ws_ln<8, 8, 4, 64>(p, stream);
+  if (k0 == 128) return launch_ws_ln<8, 4, 4, 32>(p, stream);
+  return launch_ws_ln<8, 8, 4, 32>(p, stream);
 }
 
 }  // namespace sldm
