@@ -66,30 +66,47 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(
     for (int c = 0; c < NCH; ++c) sldm::Vec<TO, V>::load(addend + row * lda + f0[c], a[c]);
   }
 
-  auto batch = [&](int k, auto u_const) {
-    constexpr int U = decltype(u_const)::value;
-    int idx[U];
+  // Column indices one batch ahead: the next 8 are loaded (clamped to the
+  // row) before the current batch's rows are summed, so the index load of
+  // batch b+1 overlaps the row loads of batch b instead of following them.
+  auto load_idx = [&](int k, int (&dst)[8]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) idx[u] = col[k + u];
+    for (int u = 0; u < 8; ++u) dst[u] = col[k + u < end ? k + u : end - 1];
+  };
+  auto batch = [&](const int* idx, auto u_const) {
+    constexpr int U = decltype(u_const)::value;
     float d[U][NCH][V];
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int c = 0; c < NCH; ++c)
         sldm::Vec<TI, V>::load(x + (int64_t)idx[u] * ldx + f0[c], d[u][c]);
+    return [&, d]() mutable {
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int c = 0; c < NCH; ++c)
+        for (int c = 0; c < NCH; ++c)
 #pragma unroll
-        for (int v = 0; v < V; ++v) acc[c][v] += d[u][c][v];
+          for (int v = 0; v < V; ++v) acc[c][v] += d[u][c][v];
+    };
   };
 
   int k = beg;
-  for (; k + 8 <= end; k += 8) batch(k, std::integral_constant<int, 8>{});
-  if (k + 4 <= end) { batch(k, std::integral_constant<int, 4>{}); k += 4; }
-  if (k + 2 <= end) { batch(k, std::integral_constant<int, 2>{}); k += 2; }
-  if (k < end) batch(k, std::integral_constant<int, 1>{});
+  if (k < end) {
+    int idx[8];
+    load_idx(k, idx);
+    for (; k + 8 <= end; k += 8) {
+      auto sum = batch(idx, std::integral_constant<int, 8>{});
+      if (k + 8 < end) load_idx(k + 8, idx);
+      sum();
+    }
+    // tail (< 8 left): indices already in idx[0 .. end-k)
+    const int left = end - k;
+    int o = 0;
+    if (left & 4) { batch(idx, std::integral_constant<int, 4>{})(); o = 4; }
+    if (left & 2) { batch(idx + o, std::integral_constant<int, 2>{})(); o += 2; }
+    if (left & 1) batch(idx + o, std::integral_constant<int, 1>{})();
+  }
 
   if (MEAN) {
     const float cnt = (float)(end - beg > 0 ? end - beg : 1);

@@ -79,8 +79,7 @@ def main():
                                                    save), a.reps)
             add(f"dense_fwd p={p_} save={save}", ms, (2 * n * f + n * f * (2 if save else 1)) * s,
                 fl)
-        for var, env in [("ws", {"SLDM_WS_FWD": "1"}),
-                         ("ws 64-row", {"SLDM_WS_FWD": "1", "SLDM_WS_LN_ROWS": "64"})]:
+        for var, env in [("ws", {"SLDM_WS_FWD": "1"})]:
             os.environ.update(env)
             ms = timeit(lambda: ops.sage_dense_fwd(agg, x, wcat, b, gam, bet, 1e-5, 0.1, 0.25, 7,
                                                    True), a.reps)
