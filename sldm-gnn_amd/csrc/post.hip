@@ -132,12 +132,13 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
   for (int64_t it = 0; it < nrounds; ++it) {
     int64_t rr[RB];
     bool live[RB];
-    float go[RB][NCH][V], xh[RB][NCH][V], zo[RB][NCH][V];
+    float go[RB][NCH][V], xh[RB][NCH][V], zo[RB][NCH][V], rsv[RB];
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
       const int64_t row = (it * RB + u) * stride + (int64_t)blockIdx.x * groups_per_block + group;
       live[u] = row < nrows;
       rr[u] = live[u] ? row : 0;
+      rsv[u] = rstd[rr[u]];   // with the row loads, not after them
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         sldm::Vec<T, V>::load(dout + rr[u] * (int64_t)feat + f0[c], go[u][c]);
@@ -148,7 +149,7 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
       const int64_t r = rr[u];
-      const float rs = rstd[r];
+      const float rs = rsv[u];
       const uint32_t rkey = sldm::dropout_row_key(seed, (uint64_t)(r + row_off));
       float gx[NCH][V], dy[NCH][V];
       float s1 = 0.0f, s2 = 0.0f;
