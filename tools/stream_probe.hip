@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <cstdlib>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
@@ -113,7 +114,7 @@ int run_rd(const uint4* a, int64_t rows, int grid, uint4* sink, const char* name
 // (2 x 16-row slabs), 8 k-steps of strided 64-B loads per slab with a ring of
 // D steps, then an epilogue burst of 2 x 8 strided 16-B stores per slab into
 // each of two [rows][256] outputs (the paired-tile store layout).
-template <int D>
+template <int D, bool CR, bool FL>
 __global__ __launch_bounds__(512) void dxpat(const uint4* __restrict__ a, uint4* __restrict__ o1,
                                              uint4* __restrict__ o2, int64_t rows, uint4* sink) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -128,7 +129,8 @@ __global__ __launch_bounds__(512) void dxpat(const uint4* __restrict__ a, uint4*
 #pragma unroll
       for (int s = 0; s < D; ++s)
 #pragma unroll
-        for (int m = 0; m < 2; ++m) v[s][m] = base[(16 * m + r16) * 32 + (s0 + s) * 4 + q];
+        for (int m = 0; m < 2; ++m)
+          v[s][m] = CR ? base[(m * D + s) * 64 + lane] : base[(16 * m + r16) * 32 + (s0 + s) * 4 + q];
 #pragma unroll
       for (int s = 0; s < D; ++s)
 #pragma unroll
@@ -141,28 +143,36 @@ __global__ __launch_bounds__(512) void dxpat(const uint4* __restrict__ a, uint4*
       const int64_t row = g * 32 + 16 * m + r16;
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        const int c = 4 * t + ((q & 1) ? 2 + (q - 1) / 2 : q / 2);   // 16-B column index
-        o1[row * 32 + c] = acc[m];
-        o2[row * 32 + c] = make_uint4(acc[m].y, acc[m].x, acc[m].w, acc[m].z);
+        if (FL) {   // 2 full 512-B rows per instruction
+          const int64_t rr = g * 32 + 16 * m + 2 * t + (lane >> 5);
+          o1[rr * 32 + (lane & 31)] = acc[m];
+          o2[rr * 32 + (lane & 31)] = make_uint4(acc[m].y, acc[m].x, acc[m].w, acc[m].z);
+        } else {
+          const int c = 4 * t + ((q & 1) ? 2 + (q - 1) / 2 : q / 2);   // 16-B column index
+          o1[row * 32 + c] = acc[m];
+          o2[row * 32 + c] = make_uint4(acc[m].y, acc[m].x, acc[m].w, acc[m].z);
+        }
       }
     }
   }
 }
 
-template <int D>
+template <int D, bool CR, bool FL>
 int run_dx(uint4* bufs[5], int64_t rows, int grid) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  dxpat<D><<<grid, 512>>>(bufs[1], bufs[2], bufs[3], rows, bufs[4]);
+  dxpat<D, CR, FL><<<grid, 512>>>(bufs[1], bufs[2], bufs[3], rows, bufs[4]);
   CK(hipEventRecord(e0));
-  for (int it = 0; it < 5; ++it) dxpat<D><<<grid, 512>>>(bufs[1], bufs[2], bufs[3], rows, bufs[4]);
+  for (int it = 0; it < 5; ++it)
+    dxpat<D, CR, FL><<<grid, 512>>>(bufs[1], bufs[2], bufs[3], rows, bufs[4]);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms = 0;
   CK(hipEventElapsedTime(&ms, e0, e1));
   ms /= 5;
-  printf("dX pattern (no MFMA)   grid %5d D %d: %.3f ms  %.0f GB/s\n", grid, D, ms,
+  printf("dX pattern (no MFMA) reads %s stores %s grid %5d D %d: %.3f ms  %.0f GB/s\n",
+         CR ? "contig" : "strided", FL ? "rows  " : "64B   ", grid, D, ms,
          rows * 1536.0 / ms / 1e6);
   return 0;
 }
@@ -175,10 +185,13 @@ int main() {
     CK(hipMalloc(&bufs[i], sz));
     CK(hipMemset(bufs[i], i, sz));
   }
-  for (int grid : {256, 512}) {
-    run_dx<4>(bufs, 10000000, grid);
-    run_dx<8>(bufs, 10000000, grid);
+  for (int rep = 0; rep < 2; ++rep) {
+    run_dx<4, false, false>(bufs, 10000000, 256);
+    run_dx<4, true, false>(bufs, 10000000, 256);
+    run_dx<4, false, true>(bufs, 10000000, 256);
+    run_dx<4, true, true>(bufs, 10000000, 256);
   }
+  if (getenv("PROBE_DX_ONLY")) return 0;
   const int64_t rows = 30000000;   // 15.4 GB: the three dY/agg/h streams of dW
   for (int grid : {256}) {
     run_rd<true, 4>(bufs[0], rows, grid, bufs[4], "read strided 64B");
