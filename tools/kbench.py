@@ -111,6 +111,43 @@ def main():
             add(f"post_bwd p={p_} zout={zo is not None}",
                 timeit(lambda: ops.post_bwd(dh, xh, rs, gam, bet, 0.1, p_, 3, dt, zout=zo),
                        a.reps), (3 + (zo is not None)) * n * f * s)
+    if want("concurrent"):
+        # forward gather and dense forward on two streams at once (independent
+        # data) vs one after the other: does overlapping them pay?
+        agg2 = torch.empty_like(agg)
+        s2 = torch.cuda.Stream()
+
+        def serial():
+            ops.gather_rows(x, gr.rowptr, gr.col, n, True, out=agg2)
+            ops.sage_dense_fwd(agg, x, wcat, b, gam, bet, 1e-5, 0.1, 0.25, 7, True)
+
+        def conc():
+            cur = torch.cuda.current_stream()
+            s2.wait_stream(cur)
+            with torch.cuda.stream(s2):
+                ops.sage_dense_fwd(agg, x, wcat, b, gam, bet, 1e-5, 0.1, 0.25, 7, True)
+            ops.gather_rows(x, gr.rowptr, gr.col, n, True, out=agg2)
+            cur.wait_stream(s2)
+
+        add("gather_fwd + dense_fwd serial", timeit(serial, a.reps), 1, 0)
+        add("gather_fwd || dense_fwd streams", timeit(conc, a.reps), 1, 0)
+        tw = torch.empty(ops.gemm_tn(dh, agg, x).shape, device=dev)
+
+        def serial_b():
+            ops.gather_rows(x, gr.rowptr, gr.col, n, False, out=agg2)
+            ops.gemm_tn(dh, agg, x)
+
+        def conc_b():
+            cur = torch.cuda.current_stream()
+            s2.wait_stream(cur)
+            with torch.cuda.stream(s2):
+                ops.gemm_tn(dh, agg, x)
+            ops.gather_rows(x, gr.rowptr, gr.col, n, False, out=agg2)
+            cur.wait_stream(s2)
+
+        add("gather_sum + gemm_tn serial", timeit(serial_b, a.reps), 1, 0)
+        add("gather_sum || gemm_tn streams", timeit(conc_b, a.reps), 1, 0)
+        del tw
     if want("torch"):
         add("torch.mm [agg|x]W^T", timeit(lambda: torch.mm(torch.cat([agg, x], 1), wcat.t()),
                                            a.reps), 3 * n * f * s, fl)
