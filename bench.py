@@ -50,7 +50,7 @@ CONFIGS = {
 }
 ZIPF_A = 0.47   # dst rank ~ k^-a over N ranks: max in-degree ~ E*(2^(1-a)-1)/(N^(1-a)-1) ~ 10k at C5
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PMC_SUMMARY = "r1c_c4_pmc_traffic.json"   # latest committed PMC passes (tools/profile_round.sh)
+PMC_SUMMARY = "r1d_c4_pmc_traffic.json"   # latest committed PMC passes (tools/profile_round.sh)
 
 
 class KernelTimer:
