@@ -111,6 +111,16 @@ def main():
             add(f"post_bwd p={p_} zout={zo is not None}",
                 timeit(lambda: ops.post_bwd(dh, xh, rs, gam, bet, 0.1, p_, 3, dt, zout=zo),
                        a.reps), (3 + (zo is not None)) * n * f * s)
+    if want("gpost"):
+        # transpose gather + the LN backward of the layer below (the fused
+        # layer boundary), and the plain transpose gather with an addend
+        xh_, rs_ = dh, torch.rand(n, device=dev) + 0.5
+        add("gather_post_bwd", timeit(lambda: ops.gather_post_bwd(
+            agg, gr.t_rowptr, gr.t_col, gr.t_order, x, xh_, rs_, gam, bet, 0.1, 0.25, 5), a.reps),
+            e * (4 + f * s) + 4 * n * f * s)
+        add("gather_bwd (sum + addend)", timeit(lambda: ops.gather_rows(
+            agg, gr.t_rowptr, gr.t_col, n, False, addend=x, order=gr.t_order), a.reps),
+            e * (4 + f * s) + 2 * n * f * s)
     if want("concurrent"):
         # forward gather and dense forward on two streams at once (independent
         # data) vs one after the other: does overlapping them pay?
