@@ -747,6 +747,33 @@ def test_gather_post_bwd_equals_gather_then_post(dtype, n, e, f, drop):
         torch.testing.assert_close(a, b, atol=1e-3, rtol=1e-4)
 
 
+@pytest.mark.parametrize("hd", [[256, 256, 256], [32, 64, 64]])
+def test_side_stream_weight_grads_bit_equal(hd, monkeypatch):
+    """SLDM_OVERLAP_DW (weight gradients on a side stream) changes only where
+    the dW kernels run: every gradient bit-equal to the serial backward."""
+    import sldm_sage.sageblock as sb
+    from sldm_sage import SageBlock
+    n, e = 20000, 160000
+    ei, x = _graph(n, e, hd[0], seed=6)
+    ei, x = ei.to(DEV), x.to(DEV, torch.bfloat16)
+    torch.manual_seed(0)
+    blk = SageBlock(hd, 0.25, 0.1).to(DEV).train()
+    gout = torch.randn(n, hd[-1], device=DEV).bfloat16()
+    res = []
+    for overlap in (False, True):
+        monkeypatch.setattr(sb, "OVERLAP_DW", overlap)
+        torch.manual_seed(9)
+        xa = x.clone().requires_grad_(True)
+        blk(xa, ei).backward(gout)
+        torch.cuda.synchronize()
+        res.append((xa.grad, {k: p.grad.clone() for k, p in blk.named_parameters()}))
+        blk.zero_grad(set_to_none=True)
+    (ga, pa), (gb, pb) = res
+    assert torch.equal(ga, gb)
+    for k in pa:
+        assert torch.equal(pa[k], pb[k]), k
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("hd", [[32, 64, 64], [16, 16, 16, 16]])
 def test_stack_fused_backward_equals_per_layer(dtype, hd):
