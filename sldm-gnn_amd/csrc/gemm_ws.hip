@@ -299,26 +299,33 @@ __global__ __launch_bounds__(kThreads) void ws_ln_kernel(WsLnArgs p) {
     const int64_t t = blockIdx.x + n * grid;
     return t < p.ntiles ? t : (int64_t)blockIdx.x;
   };
+  // Per-lane DMA offsets of a full tile, computed once (tile-invariant); a
+  // final partial tile recomputes them with its rows clamped to M-1.
+  uint32_t voff0[DPW];
+  auto dma_off = [&](int j, int64_t last) -> uint32_t {
+    const int d = wave * DPW + j;
+    const bool sub1 = d * 1024 >= SUB1;
+    const int ob = sub1 ? d * 1024 - SUB1 : d * 1024;
+    const int gsub = (sub1 ? RB1 : RB0) / 16;
+    const int gp = ob / 16 + lane;
+    const int r = gp / gsub, jg = gp % gsub;
+    const int64_t rr = r < last ? r : last;
+    return (uint32_t)(rr * (sub1 ? p.lda1 : p.lda0) * 2 + 16 * (jg ^ (r & 15)));
+  };
+#pragma unroll
+  for (int j = 0; j < DPW; ++j) voff0[j] = dma_off(j, TM);
   auto issue = [&](int64_t n) {
     const int64_t r0 = tile_of(n) * TM;
     const int64_t last = p.M - 1 - r0;
-    int ln;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
 #pragma unroll
     for (int j = 0; j < DPW; ++j) {
       const int d = wave * DPW + j;                 // wave-uniform
       const bool sub1 = d * 1024 >= SUB1;
-      const int ob = sub1 ? d * 1024 - SUB1 : d * 1024;
-      const int gsub = (sub1 ? RB1 : RB0) / 16;     // granules per sub-tile row
-      const int gp = ob / 16 + ln;
-      const int r = gp / gsub, jg = gp % gsub;
-      const int64_t rr = r < last ? r : last;
       const char* base = reinterpret_cast<const char*>(sub1 ? p.a1 + r0 * p.lda1
                                                             : p.a0 + r0 * p.lda0);
-      const int64_t lda = sub1 ? p.lda1 : p.lda0;
       uint32_t la = lds0 + (uint32_t)((n % NBUF) * TB + d * 1024);
       asm volatile("" : "+s"(base), "+s"(la));
-      dma16(base, (uint32_t)(rr * lda * 2 + 16 * (jg ^ (r & 15))), la);
+      dma16(base, last >= TM - 1 ? voff0[j] : dma_off(j, last), la);
     }
   };
 
@@ -356,22 +363,31 @@ __global__ __launch_bounds__(kThreads) void ws_ln_kernel(WsLnArgs p) {
     asm volatile("" ::: "memory");
     issue(n + NBUF - 1);
 
-    const char* slot = smem + (n % NBUF) * TB;
     f4v acc[RG][CT];
 #pragma unroll
     for (int m = 0; m < RG; ++m)
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) acc[m][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+    // B-fragment addresses: (4 ls + q) ^ i = 4 (ls ^ (i >> 2)) + ((q ^ i) & 3)
+    // for ls = 4a + b, so a lane's address is one of 4 per-lane values (b)
+    // plus compile-time offsets (a, m, sub-tile) -- no per-read VALU.
+    typedef __attribute__((address_space(3))) const s8v* lds_frag;
+    const uint32_t sl = lds0 + (uint32_t)((n % NBUF) * TB);
+    uint32_t lb0[4], lb1[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t o = (uint32_t)(64 * (b ^ (i >> 2)) + 16 * ((q ^ i) & 3));
+      lb0[b] = sl + (uint32_t)(i * RB0) + o;
+      lb1[b] = sl + (uint32_t)(SUB1 + i * RB1) + o;
+    }
     s8v bf[2][RG];
     auto read_b = [&](int s, s8v (&dst)[RG]) {
       const bool s1 = s >= K0STEPS;
       const int ls = s1 ? s - K0STEPS : s;
-      const char* sb = slot + (s1 ? SUB1 : 0);
       const int rb = s1 ? RB1 : RB0;
-      const int goff = 16 * ((4 * ls + q) ^ i);
+      const uint32_t a = (s1 ? lb1 : lb0)[ls & 3] + (uint32_t)(256 * (ls >> 2));
 #pragma unroll
-      for (int m = 0; m < RG; ++m)
-        dst[m] = *reinterpret_cast<const s8v*>(sb + (16 * m + i) * rb + goff);
+      for (int m = 0; m < RG; ++m) dst[m] = *(lds_frag)(uintptr_t)(a + (uint32_t)(16 * m * rb));
     };
     read_b(0, bf[0]);
 #pragma unroll
