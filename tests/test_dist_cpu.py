@@ -89,15 +89,17 @@ def _run(world, n, hdims, strategy, chunks=4):
         assert msg == "ok", f"rank {rank}:\n{msg}"
 
 
-@pytest.mark.parametrize("world,n", [(2, 300), (3, 301), (4, 97)])
+@pytest.mark.parametrize("world,n", [(2, 300), (3, 301), (4, 97), (8, 203)])
 def test_dist_sageblock_matches_single_device(world, n):
     _run(world, n, [8, 12, 8], "halo")
 
 
-@pytest.mark.parametrize("world,n,chunks", [(2, 300, 4), (3, 301, 3), (4, 97, 1), (4, 10, 8)])
+@pytest.mark.parametrize("world,n,chunks", [(2, 300, 4), (3, 301, 3), (4, 97, 1), (4, 10, 8),
+                                             (8, 203, 4)])
 def test_feature_sliced_sageblock_matches_single_device(world, n, chunks):
     # F = 8 and 12 over 3-4 ranks: uneven column slices; n = 10 at 4 ranks
-    # with 8 chunks: empty chunks on some ranks
+    # with 8 chunks: empty chunks on some ranks; 8 ranks (the scaling run's
+    # width): one or two columns per rank
     _run(world, n, [8, 12, 8], "feature", chunks)
 
 
