@@ -156,6 +156,10 @@ def main():
                     choices=["auto", "halo", "feature", "replicate"],
                     help="multi-GPU partition: destination rows + halo exchange, feature "
                          "slices + layout all-to-alls, or the lower modelled time (default)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, one GPU per rank: the measured path) or gloo "
+                         "(rehearsal of the N>1 flow with several ranks sharing the GPUs of "
+                         "a smaller box; its times are not a measurement)")
     args = ap.parse_args()
 
     if args.graph is None:
@@ -166,13 +170,18 @@ def main():
     use_dist = world > 1 or args.force_dist
     if use_dist:
         import torch.distributed as dist
+        # one GPU per rank (RCCL); a gloo rehearsal may put several ranks on one GPU
+        local_rank %= torch.cuda.device_count()
         torch.cuda.set_device(local_rank)
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29533")
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local_rank)
 
     from sldm_sage import SageBlock, graph_cache, ops
@@ -338,6 +347,9 @@ def main():
         }
         if variant is not None:
             line["locality_variant"] = variant
+        if use_dist and args.dist_backend != "nccl":
+            line["rehearsal"] = (f"{args.dist_backend} backend, ranks sharing "
+                                 f"{torch.cuda.device_count()} GPU(s): flow check, not a measurement")
         print(json.dumps(line), flush=True)
     if use_dist:
         torch.distributed.destroy_process_group()
