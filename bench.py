@@ -20,7 +20,9 @@ The JSON line also carries ``roofline`` for the dominant kernel (the CSR
 gather-mean: the SageBlock scatter-add), measured with HIP events around
 every launch on the launch stream inside the timed region, and
 ``cpu_baseline``: the CPU oracle (oracle/sage_ref.py, the reference's ATen op
-sequence) timed on this host on a bounded sample (rank 0, N=1 only).
+sequence) timed on this host on a bounded sample (rank 0, N=1 only), and
+``step_roofline`` (N=1): T* = the algorithmic bytes of every timed kernel of a
+step / 8 TB/s + the step's GEMM FLOP / the dense MFMA peak, as T*/t_step.
 """
 from __future__ import annotations
 
@@ -50,6 +52,8 @@ CONFIGS = {
 }
 ZIPF_A = 0.47   # dst rank ~ k^-a over N ranks: max in-degree ~ E*(2^(1-a)-1)/(N^(1-a)-1) ~ 10k at C5
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_COPY_GBS = 6290.0   # measured float4-copy ceiling (MI355X_MICROARCH.md)
+MFMA_PEAK_TFLOPS = {torch.bfloat16: 2500.0, torch.float32: 157.3}   # dense, same guide
 PMC_SUMMARY = "r1d_c4_pmc_traffic.json"   # latest committed PMC passes (tools/profile_round.sh)
 
 
@@ -256,12 +260,16 @@ def main():
         barrier()
         if timed_kernels:
             ops.set_timing_hook(timer)
+        marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        marks[0].record()
+        for i in range(args.steps):
             blk.zero_grad(set_to_none=True)
             step()
+            marks[i + 1].record()
         barrier()
         elapsed = time.perf_counter() - t0
+        step_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)]
         ops.set_timing_hook(None)
         if world > 1:
             tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -278,15 +286,15 @@ def main():
             step()
             barrier()
             incl = e * L / (time.perf_counter() - t1)
-        return elapsed, timer.summary(), dist_info, incl
+        return elapsed, timer.summary(), dist_info, incl, step_ms
 
-    elapsed, kern, dist_info, incl = run(args.graph, True)
+    elapsed, kern, dist_info, incl, step_ms = run(args.graph, True)
     variant = None
     if world > 1 and args.graph == "uniform":
         # also the locality-structured variant (block-community
         # graph, cut fraction stated) -- the regime where the exchange overlaps.
         torch.cuda.empty_cache()
-        v_el, _, v_info, _ = run("local", False)
+        v_el, _, v_info, _, _ = run("local", False)
         variant = dict(graph="local", value=round(e * L * args.steps / v_el, 1),
                        ms_per_step=round(v_el / args.steps * 1e3, 3), **v_info)
         torch.cuda.empty_cache()
@@ -313,6 +321,21 @@ def main():
                     kernel="gather_rows_kernel (forward mean aggregation)",
                     avg_ms=round(g["avg_ms"], 4), launches=g["launches"],
                     bytes_per_launch=int(g["avg_bytes"]))
+    # SURVEY.md §8d full-step roofline: T* = (algorithmic bytes of every timed
+    # kernel in a step) / HBM peak + (GEMM FLOP of a step) / dense MFMA peak,
+    # reported as T*/t (N = 1; at N > 1 the per-rank work is not the whole graph).
+    step_bytes = sum(v["avg_bytes"] * v["launches"] for v in kern.values()) / args.steps
+    step_roof = None
+    if kern and not use_dist:
+        flop = 3 * 2.0 * n * 2 * f * f * L        # fwd, dX, dW of [N,2F]x[2F,F] per layer
+        t_star = step_bytes / (HBM_PEAK_GBS * 1e9) + flop / (MFMA_PEAK_TFLOPS[dtype] * 1e12)
+        t_star_copy = step_bytes / (HBM_COPY_GBS * 1e9) + flop / (MFMA_PEAK_TFLOPS[dtype] * 1e12)
+        step_roof = dict(bytes_per_step=int(step_bytes), flop_per_step=flop,
+                         t_star_ms=round(t_star * 1e3, 3),
+                         frac=round(t_star / (elapsed / args.steps), 4),
+                         frac_vs_measured_copy=round(t_star_copy / (elapsed / args.steps), 4),
+                         note="T* = bytes/8 TB/s + FLOP/dense MFMA peak (SURVEY 8d); "
+                              "frac_vs_measured_copy prices bytes at the 6.29 TB/s copy ceiling")
     kernels = {k: dict(avg_ms=round(v["avg_ms"], 4), launches=v["launches"],
                        gbs=round(v["avg_bytes"] / (v["avg_ms"] * 1e-3) / 1e9, 1))
                for k, v in kern.items()}
@@ -340,7 +363,10 @@ def main():
                        "layers": L, "dropout": 0.25, "negative_slope": 0.1,
                        "parallelism": (_parallelism(dist_info.get("strategy"), world)
                                        if use_dist else "single"), **dist_info},
+            "graph_edges_per_s": round(e * args.steps / elapsed, 1),
+            "ms_per_step_median_rank0": round(statistics.median(step_ms), 3),
             "value_incl_csr_build": round(incl, 1) if incl else None,
+            "step_roofline": step_roof,
             "roofline": roof,
             "kernels": kernels,
             "cpu_baseline": base,
