@@ -760,6 +760,18 @@ def _remote_unique(ids: torch.Tensor, r0: int, r1: int) -> int:
 _DENSE_BYTES_PER_ROW_FS = 13.0
 _DENSE_BPS = 4.0e12
 _FEAT_CHUNKS = 4          # partition_features' default pipeline depth
+# A partition is chosen only when the model has it faster than one GPU doing
+# all the work (replicate) by this factor: the xGMI and kernel rates above are
+# estimates (~ +-20 %), and a strong-scaling run slower than one GPU is the
+# outcome to rule out (C4 uniform at W = 4: feature 32.0 vs 34.8 ms per layer
+# modelled -> replicate; at W = 8: 9.0 vs 34.8 -> feature).
+_PARTITION_MARGIN = 1.2
+
+
+def choose_strategy(info: dict) -> str:
+    """The planner's pick from :func:`estimate_strategies`' modelled times."""
+    best = min(("halo", "feature"), key=lambda k: info[f"{k}_s"])
+    return best if info[f"{best}_s"] * _PARTITION_MARGIN < info["replicate_s"] else "replicate"
 
 
 def estimate_strategies(edge_index: torch.Tensor, num_nodes: int, world: int, rank: int,
@@ -841,7 +853,7 @@ def plan_partition(edge_index: torch.Tensor, num_nodes: int, world: int, rank: i
                    feat: int, elem: int, strategy: str = "auto", backend=HipBackend,
                    group=None, chunks: int = 4):
     """Partition with ``strategy`` in {"auto", "halo", "feature", "replicate"};
-    "auto" takes the lowest modelled time of :func:`estimate_strategies`
+    "auto" takes :func:`choose_strategy` of :func:`estimate_strategies`
     (every rank gets the same answer: the estimate is max-reduced).  Returns
     (partition, info).  With "replicate" every rank runs the whole graph: the
     caller passes all rows of x (``partition.row_begin/row_end`` span them)."""
@@ -851,7 +863,7 @@ def plan_partition(edge_index: torch.Tensor, num_nodes: int, world: int, rank: i
             strategy = "halo"
         else:
             info = estimate_strategies(edge_index, num_nodes, world, rank, feat, elem, group)
-            strategy = min(("halo", "feature", "replicate"), key=lambda k: info[f"{k}_s"])
+            strategy = choose_strategy(info)
     info["strategy"] = strategy
     if strategy == "feature":
         return partition_features(edge_index, num_nodes, world, rank, backend, chunks), info

@@ -110,10 +110,12 @@ def test_auto_strategy_matches_single_device(world):
 
 def test_planner_choices_on_c4_shapes():
     """The cost model at C4's shape (scaled 1/10): a uniform random graph is
-    replicated at W = 2 (one xGMI link cannot beat one GPU) and feature-sliced
-    at W = 8; a partition-local graph takes the halo path at W = 8."""
+    replicated at W = 2 (one xGMI link cannot beat one GPU) and at W = 4 (the
+    feature path is modelled only ~8 % faster, inside the planner's margin),
+    feature-sliced at W = 8; a partition-local graph takes the halo path at
+    W = 4 and 8."""
     import torch.distributed as dist
-    from sldm_sage.dist import estimate_strategies
+    from sldm_sage.dist import choose_strategy, estimate_strategies
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     dist.init_process_group("gloo", rank=0, world_size=1)
     try:
@@ -126,12 +128,13 @@ def test_planner_choices_on_c4_shapes():
         local_src = torch.where(torch.rand(e, generator=g) < 0.9, loc.clamp(max=n - 1), src)
 
         def pick(edges, w):
-            r = estimate_strategies(edges, n, w, 0, f, 2)
-            return min(("halo", "feature", "replicate"), key=lambda k: r[f"{k}_s"])
+            return choose_strategy(estimate_strategies(edges, n, w, 0, f, 2))
 
         uni = torch.stack([src, dst])
         assert pick(uni, 2) == "replicate"
+        assert pick(uni, 4) == "replicate"
         assert pick(uni, 8) == "feature"
+        assert pick(torch.stack([local_src, dst]), 4) == "halo"
         assert pick(torch.stack([local_src, dst]), 8) == "halo"
     finally:
         dist.destroy_process_group()

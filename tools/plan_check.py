@@ -13,7 +13,7 @@ import torch.distributed as dist  # noqa: E402
 def main():
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29611")
     dist.init_process_group("gloo", rank=0, world_size=1)
-    from sldm_sage.dist import estimate_strategies
+    from sldm_sage.dist import choose_strategy, estimate_strategies
     n, e, f = 1_000_000, 10_000_000, 256
     g = torch.Generator().manual_seed(0)
     ei = torch.stack([torch.randint(0, n, (e,), generator=g),
@@ -26,7 +26,7 @@ def main():
     for name, edges in (("uniform", ei), ("local", eil)):
         for w in (2, 4, 8):
             r = estimate_strategies(edges, n, w, 0, f, 2)
-            best = min(("halo", "feature", "replicate"), key=lambda k: r[f"{k}_s"])
+            best = choose_strategy(r)
             print(name, w, {k: round(v * 1e4, 2) for k, v in r.items() if k.endswith("_s")},
                   "->", best, flush=True)
     dist.destroy_process_group()
