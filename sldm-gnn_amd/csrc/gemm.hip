@@ -130,6 +130,108 @@ __device__ __forceinline__ typename NtOps<T>::Frag nt_load_b(const NtArgs<T>& p,
   return f;
 }
 
+// Row epilogue of an NT tile whose fp32 accumulators sit in LDS [BM][ldc]:
+// a wave owns a row; lane holds columns 4*lane .. 4*lane+3 (4 waves per block).
+template <typename T, int MODE>
+__device__ __forceinline__ void nt_row_epilogue(const NtArgs<T>& p, const float* smem, int ldc,
+                                                int64_t m0, int n0, int BM, int wave, int lane) {
+  const int bn_valid = min(16 * p.ct, p.Nc - n0);
+  // A row per 32 lanes when it has <= 128 columns (two rows per wave step; the
+  // 32-lane sums equal the 64-lane ones, whose upper half added zeros), else
+  // per 64 lanes.
+  const int lpr = bn_valid > 128 ? 64 : 32;
+  const int rpi = 64 / lpr;
+  const int c0 = 4 * (lane & (lpr - 1));
+  const bool lane_on = c0 < bn_valid;
+  const bool full4 = (c0 + 3 < bn_valid) && (p.ldo % 4 == 0);
+  // The lane's columns are fixed: bias / gamma / beta are loaded once, not per
+  // row (per-row loads put three dependent L1 round trips on every row).
+  float bi[4] = {0.f, 0.f, 0.f, 0.f}, ga[4] = {0.f, 0.f, 0.f, 0.f}, be[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (MODE == EPI_LN) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = min(c0 + j, bn_valid - 1);
+      if (p.bias) bi[j] = p.bias[c];
+      ga[j] = p.gamma[c];
+      be[j] = p.beta[c];
+    }
+  }
+  for (int rr = wave * rpi + lane / lpr; rr < BM; rr += 4 * rpi) {
+    const int64_t row = m0 + rr;
+    if (row >= p.M) break;   // uniform per row group (the sums stay inside it)
+    float v[4];
+    {
+      const f4v t4 = *reinterpret_cast<const f4v*>(&smem[rr * ldc + c0]);
+      v[0] = t4[0]; v[1] = t4[1]; v[2] = t4[2]; v[3] = t4[3];
+    }
+    if constexpr (MODE == EPI_LN) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = c0 + j;
+        const bool ok = lane_on && c < bn_valid;
+        v[j] = ok ? v[j] + bi[j] : 0.f;
+        s += v[j];
+      }
+      const float inv_n = 1.0f / (float)p.Nc;
+      const float mean = sldm::group_sum(s, lpr) * inv_n;
+      float sq = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = (lane_on && c0 + j < bn_valid) ? v[j] - mean : 0.f;
+        sq += d * d;
+      }
+      const float rstd = 1.0f / sqrtf(sldm::group_sum(sq, lpr) * inv_n + p.eps);
+      if (p.rstd && (lane & (lpr - 1)) == 0) p.rstd[row] = rstd;
+      if (!lane_on) continue;
+      const uint32_t rkey = sldm::dropout_row_key(p.seed, (uint64_t)(row + p.row_off));
+      float xh[4], z[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = min(c0 + j, bn_valid - 1);
+        xh[j] = (v[j] - mean) * rstd;
+        const float y = __builtin_fmaf(xh[j], ga[j], be[j]);   // as post_bwd recomputes it
+        float a = y > 0.f ? y : y * p.slope;
+        if (p.drop_p > 0.f) {
+          a = sldm::dropout_keep(rkey, (uint32_t)c, sldm::dropout_threshold(p.drop_p))
+                  ? a * p.drop_scale : 0.f;
+        }
+        z[j] = a;
+      }
+      T* orow = p.out + row * p.ldo + n0 + c0;
+      T* xrow = p.xhat ? p.xhat + row * p.ldo + n0 + c0 : nullptr;
+      if (full4) {
+        sldm::Vec<T, 4>::store(orow, z);
+        if (xrow) sldm::Vec<T, 4>::store(xrow, xh);
+      } else {
+        for (int j = 0; j < 4 && c0 + j < bn_valid; ++j) {
+          sldm::Vec<T, 1>::store(orow + j, &z[j]);
+          if (xrow) sldm::Vec<T, 1>::store(xrow + j, &xh[j]);
+        }
+      }
+    } else {
+      if (!lane_on) continue;
+      if (p.rowptr) {
+        const int deg = p.rowptr[row + 1] - p.rowptr[row];
+        const float cnt = (float)(deg > 0 ? deg : 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (n0 + c0 + j < p.scale_cols) v[j] = v[j] / cnt;
+      }
+      // split output: columns >= scale_cols go to out2 (scale_cols % 4 == 0,
+      // so a 4-column group never straddles the split)
+      const bool hi = p.out2 && n0 + c0 >= p.scale_cols;
+      T* orow = hi ? p.out2 + row * p.ldo2 + (n0 + c0 - p.scale_cols)
+                   : p.out + row * p.ldo + n0 + c0;
+      if (full4) {
+        sldm::Vec<T, 4>::store(orow, v);
+      } else {
+        for (int j = 0; j < 4 && c0 + j < bn_valid; ++j) sldm::Vec<T, 1>::store(orow + j, &v[j]);
+      }
+    }
+  }
+}
+
 // Row tile (16·MT rows) and resident blocks per CU.  fp32 (exact
 // v_mfma_f32_16x16x4_f32, 16x slower per FLOP than bf16) is MFMA-bound and
 // hides its per-k-step weight-fragment loads (L2) only with more waves in
@@ -295,85 +397,145 @@ __global__ __launch_bounds__(kBlock, NtTile<T>::MINB) void gemm_nt_kernel(NtArgs
   }
   __syncthreads();
 
-  // Row epilogue: a wave owns a row; lane holds columns 4*lane .. 4*lane+3.
-  const int bn_valid = min(16 * p.ct, p.Nc - n0);
-  const int c0 = 4 * lane;
-  const bool lane_on = c0 < bn_valid;
-  const bool full4 = (c0 + 3 < bn_valid) && (p.ldo % 4 == 0);
-  for (int rr = wave; rr < BM; rr += 4) {
-    const int64_t row = m0 + rr;
-    if (row >= p.M) break;
-    float v[4];
-    {
-      const f4v t4 = *reinterpret_cast<const f4v*>(&smem[rr * ldc + c0]);
-      v[0] = t4[0]; v[1] = t4[1]; v[2] = t4[2]; v[3] = t4[3];
-    }
-    if constexpr (MODE == EPI_LN) {
-      float s = 0.f;
+  nt_row_epilogue<T, MODE>(p, smem, ldc, m0, n0, BM, wave, lane);
+}
+
+// fp32 weight-stationary NT (exact-fp32 LN forward and dX with one column
+// block, Nc <= 256, K = KC in {128, 256}; C2's shapes).  The tile kernel above
+// re-reads its weight fragments from L2 every k-step and stages each A tile
+// with a full load -> barrier -> compute sequence, so its MFMAs idle while
+// loads are in flight (PMC: ~30 % MFMA-busy).  Here every wave loads its
+// weight fragments once (<= 128 VGPRs) and the block walks 32-row tiles
+// persistently: the next tile's A loads are issued right after the current
+// tile lands in LDS and stay in flight under the MFMAs, which touch no
+// vector memory.  Same k and sub-step order per accumulator as the tile
+// kernel: bit-identical outputs.
+template <int TPW, int KC, int MODE>
+__global__ __launch_bounds__(kBlock, 2) void gemm_nt_ws32_kernel(NtArgs<float> p,
+                                                                  int64_t ntiles) {
+  using O = NtOps<float>;
+  constexpr int MT = 2, BM = 32;
+  constexpr int KSTEPS = KC / O::KS;
+  constexpr int VPR = KC / 4;               // 16-B vectors per A row
+  constexpr int NV = BM * VPR / kBlock;     // per thread per tile
+  static_assert(BM * VPR % kBlock == 0 && KSTEPS * TPW <= 32, "ws32 shape");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int PA = KC + 4;                // A row pitch (floats): 16 B mod 256 B
+  float* lds_a = smem;
+  float* lds_c = smem + BM * PA;
+  const int ldc = 16 * p.ct + 4;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q = lane >> 4, r16 = lane & 15;
+
+  int64_t tile = blockIdx.x;
+  if (tile >= ntiles) return;
+
+  bool tval[TPW];
+  f4v bw[KSTEPS][TPW];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = c0 + j;
-        const bool ok = lane_on && c < bn_valid;
-        v[j] = ok ? v[j] + (p.bias ? p.bias[c] : 0.f) : 0.f;
-        s += v[j];
-      }
-      const float inv_n = 1.0f / (float)p.Nc;
-      const float mean = sldm::group_sum(s, 64) * inv_n;
-      float sq = 0.f;
+  for (int t = 0; t < TPW; ++t) {
+    const int tid = wave + 4 * t;
+    tval[t] = tid < p.ct;
+    const int c = 16 * tid + r16;
+    const int bc = c < p.Nc ? c : p.Nc - 1;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float d = (lane_on && c0 + j < bn_valid) ? v[j] - mean : 0.f;
-        sq += d * d;
-      }
-      const float rstd = 1.0f / sqrtf(sldm::group_sum(sq, 64) * inv_n + p.eps);
-      if (p.rstd && lane == 0) p.rstd[row] = rstd;
-      if (!lane_on) continue;
-      const uint32_t rkey = sldm::dropout_row_key(p.seed, (uint64_t)(row + p.row_off));
-      float xh[4], z[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = min(c0 + j, bn_valid - 1);
-        xh[j] = (v[j] - mean) * rstd;
-        const float y = __builtin_fmaf(xh[j], p.gamma[c], p.beta[c]);   // as post_bwd recomputes it
-        float a = y > 0.f ? y : y * p.slope;
-        if (p.drop_p > 0.f) {
-          a = sldm::dropout_keep(rkey, (uint32_t)c, sldm::dropout_threshold(p.drop_p))
-                  ? a * p.drop_scale : 0.f;
-        }
-        z[j] = a;
-      }
-      T* orow = p.out + row * p.ldo + n0 + c0;
-      T* xrow = p.xhat ? p.xhat + row * p.ldo + n0 + c0 : nullptr;
-      if (full4) {
-        sldm::Vec<T, 4>::store(orow, z);
-        if (xrow) sldm::Vec<T, 4>::store(xrow, xh);
-      } else {
-        for (int j = 0; j < 4 && c0 + j < bn_valid; ++j) {
-          sldm::Vec<T, 1>::store(orow + j, &z[j]);
-          if (xrow) sldm::Vec<T, 1>::store(xrow + j, &xh[j]);
-        }
-      }
-    } else {
-      if (!lane_on) continue;
-      if (p.rowptr) {
-        const int deg = p.rowptr[row + 1] - p.rowptr[row];
-        const float cnt = (float)(deg > 0 ? deg : 1);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (n0 + c0 + j < p.scale_cols) v[j] = v[j] / cnt;
-      }
-      // split output: columns >= scale_cols go to out2 (scale_cols % 4 == 0,
-      // so a 4-column group never straddles the split)
-      const bool hi = p.out2 && n0 + c0 >= p.scale_cols;
-      T* orow = hi ? p.out2 + row * p.ldo2 + (n0 + c0 - p.scale_cols)
-                   : p.out + row * p.ldo + n0 + c0;
-      if (full4) {
-        sldm::Vec<T, 4>::store(orow, v);
-      } else {
-        for (int j = 0; j < 4 && c0 + j < bn_valid; ++j) sldm::Vec<T, 1>::store(orow + j, &v[j]);
-      }
-    }
+    for (int ks = 0; ks < KSTEPS; ++ks) bw[ks][t] = nt_load_b<float, true>(p, bc, ks * O::KS + 4 * q);
   }
+
+  f4v st[NV];
+  auto load_tile = [&](int64_t tl) {
+    const int64_t m0 = tl * BM;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = threadIdx.x + i * kBlock;
+      const int r = v / VPR, kv = (v - r * VPR) * 4;
+      const int64_t row = min(m0 + r, p.M - 1);
+      const float* src = kv < p.k0 ? p.a0 + row * p.lda0 + kv : p.a1 + row * p.lda1 + (kv - p.k0);
+      st[i] = *reinterpret_cast<const f4v*>(src);
+    }
+  };
+  load_tile(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    // lds_a is free: every wave passed the barrier after the previous tile's MFMAs
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = threadIdx.x + i * kBlock;
+      const int r = v / VPR, kv = (v - r * VPR) * 4;
+      *reinterpret_cast<f4v*>(lds_a + r * PA + kv) = st[i];
+    }
+    __syncthreads();
+    if (tile + gridDim.x < ntiles) load_tile(tile + gridDim.x);
+
+    f4v acc[MT][TPW];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) acc[m][t] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ++ks) {
+      f4v a[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        a[m] = *reinterpret_cast<const f4v*>(lds_a + (16 * m + r16) * PA + ks * O::KS + 4 * q);
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        if (!tval[t]) continue;
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][c], bw[ks][t][c], acc[m][t], 0, 0, 0);
+      }
+    }
+    // lds_c is free: every wave passed this tile's first barrier after its
+    // previous epilogue
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      if (!tval[t]) continue;
+      const int c = 16 * (wave + 4 * t) + r16;
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lds_c[(16 * m + 4 * q + r) * ldc + c] = acc[m][t][r];
+    }
+    __syncthreads();
+    nt_row_epilogue<float, MODE>(p, lds_c, ldc, tile * BM, 0, BM, wave, lane);
+  }
+}
+
+template <int TP, int KCV, int MODE>
+int launch_ws32_t(const NtArgs<float>& p, int64_t ntiles, int64_t grid, size_t lds,
+                  hipStream_t stream) {
+  auto kern = gemm_nt_ws32_kernel<TP, KCV, MODE>;
+  if (lds > 65536)
+    SLDM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  kern<<<(unsigned)grid, kBlock, lds, stream>>>(p, ntiles);
+  SLDM_LAUNCH_CHECK("gemm_nt_ws32_kernel");
+  return SLDM_OK;
+}
+
+// Returns -1 when the shape is not one the fp32 weight-stationary kernel takes
+// (the tile kernel runs it), else the launch status.  SLDM_NT_WS32=0 disables.
+template <int MODE>
+int launch_nt_ws32(const NtArgs<float>& p, int tpw, hipStream_t stream) {
+  const char* e = getenv("SLDM_NT_WS32");
+  const bool enabled = !(e && e[0] == '0');
+  auto mis = [](const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) != 0; };
+  if (!enabled || p.M <= 0 || p.grid_y != 1 || !(p.K == 128 || p.K == 256) || p.k0 % 4 ||
+      p.lda0 % 4 || p.lda1 % 4 || p.ldb % 4 || mis(p.a0) || (p.K > p.k0 && mis(p.a1)) || mis(p.b))
+    return -1;
+  const int64_t ntiles = (p.M + 31) / 32;
+  const int64_t grid = ntiles < 512 ? ntiles : 512;   // 2 blocks x 256 CUs, persistent
+  const size_t lds = sizeof(float) * (32 * (size_t)(p.K + 4) + 32 * (size_t)(16 * p.ct + 4));
+  if (p.K == 256 && tpw == 1) return launch_ws32_t<1, 256, MODE>(p, ntiles, grid, lds, stream);
+  if (p.K == 256 && tpw == 2) return launch_ws32_t<2, 256, MODE>(p, ntiles, grid, lds, stream);
+  if (p.K == 128 && tpw == 1) return launch_ws32_t<1, 128, MODE>(p, ntiles, grid, lds, stream);
+  if (p.K == 128 && tpw == 2) return launch_ws32_t<2, 128, MODE>(p, ntiles, grid, lds, stream);
+  if (p.K == 128 && tpw == 3) return launch_ws32_t<3, 128, MODE>(p, ntiles, grid, lds, stream);
+  if (p.K == 128 && tpw == 4) return launch_ws32_t<4, 128, MODE>(p, ntiles, grid, lds, stream);
+  return -1;
 }
 
 template <typename T, int TPW, bool VEC, int MODE>
@@ -419,6 +581,10 @@ int launch_nt(NtArgs<T>& p, hipStream_t stream) {
                    (k1 == 0 || p.lda1 % EPL == 0) && (p.ldb % EPL == 0) && al(p.a0) &&
                    (k1 == 0 || al(p.a1)) && al(p.b) && (p.K % KS == 0);
   const int tpw = (p.ct + 3) / 4;
+  if constexpr (sizeof(T) == 4) {
+    const int rc = launch_nt_ws32<MODE>(p, tpw, stream);
+    if (rc >= 0) return rc;
+  }
 #define SLDM_NT_CASE(TP)                                                        \
   case TP:                                                                      \
     return vec ? launch_nt_t<T, TP, true, MODE>(p, stream)                      \

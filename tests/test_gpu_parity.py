@@ -243,9 +243,9 @@ def test_layer_backward_chain(dtype, fi, fo):
 def test_dropout_statistics_and_backward_mask():
     from sldm_sage import ops
     n, f, p = 4096, 128, 0.25
-    h = torch.randn(n, f, device=DEV)
+    h = torch.randn(n, f, device=DEV, generator=torch.Generator(device=DEV).manual_seed(5))
     gam = torch.ones(f, device=DEV)
-    bet = torch.full((f,), 5.0, device=DEV)          # y > 0 everywhere
+    bet = torch.full((f,), 8.0, device=DEV)          # y > 0 everywhere (xhat > -8: seeded)
     out, xhat, rstd = ops.post_fwd(h, None, gam, bet, 1e-5, 0.1, p, 1234, torch.float32, True)
     kept = out != 0
     rate = kept.float().mean().item()
@@ -687,6 +687,40 @@ def test_ws_gemm_rowscale_bit_exact_vs_stream(m, fi, monkeypatch):
         torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
         split = run(True, rowptr, True)
         assert torch.equal(split, got)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m", [1, 31, 33, 1000, 20011])
+@pytest.mark.parametrize("f", [64, 96, 128])
+def test_fp32_ws32_nt_bit_exact_vs_tile(m, f, monkeypatch):
+    """gemm_nt_ws32_kernel (fp32, weights held in VGPRs, persistent 32-row
+    tiles with the next tile's loads under the MFMAs) runs the tile kernel's
+    per-accumulator MFMA order: LN forward (K = 2f, with dropout, saved xhat
+    and rstd) and dX (K = f, Nc = 2f, 1/deg on the first f columns, split and not)
+    equal bit for bit with SLDM_NT_WS32=0; ragged last tiles and tiles fewer
+    than the persistent grid included."""
+    from sldm_sage import build_graph, ops
+    from oracle.sage_ref import random_graph
+    ei, _ = random_graph(m, 3 * m + 1, 1, seed=m + f)
+    g = build_graph(ei.to(DEV), m)
+    gen = torch.Generator(device=DEV).manual_seed(m * 7 + f)
+    agg = torch.randn(m, f, generator=gen, device=DEV)
+    x = torch.randn(m, f, generator=gen, device=DEV)
+    wcat = torch.randn(f, 2 * f, generator=gen, device=DEV) / (2 * f) ** 0.5
+    b, gam, bet = (torch.randn(f, generator=gen, device=DEV) for _ in range(3))
+    dh = torch.randn(m, f, generator=gen, device=DEV)
+    wt = torch.randn(2 * f, f, generator=gen, device=DEV) / f ** 0.5
+
+    def run(ws):
+        monkeypatch.setenv("SLDM_NT_WS32", "1" if ws else "0")
+        fwd = ops.sage_dense_fwd(agg, x, wcat, b, gam, bet, 1e-5, 0.1, 0.25, 5, True)
+        dx = ops.gemm_nt_rowscale(dh, wt, g.rowptr, f)
+        dxs = ops.gemm_nt_rowscale(dh, wt, g.rowptr, f, split=True)
+        torch.cuda.synchronize()
+        return [*fwd, dx, *dxs]
+
+    for a, c in zip(run(True), run(False)):
+        assert torch.equal(a, c)
 
 
 # ------------------------------------------------ overlapped (split) gather --
