@@ -100,11 +100,12 @@ template <> struct Vec<uint16_t, 1> {
 };
 
 // 16-B vector load / store with an optional non-temporal hint, for the gathers
-// over tables far larger than the 256 MB Infinity Cache: with both the random
-// source-row loads and the output stores non-temporal, the C4 forward gather
-// runs 9.6 -> 9.0 ms and the transpose gather 10.5 -> 9.7 ms (same-box A/B;
-// the loads alone are slower, the stores alone gain half).  Other widths fall
-// back to Vec.
+// over tables far larger than the 256 MB Infinity Cache.  Same-box A/B of the
+// C4 bench (nt_gather below): output stores non-temporal gain 2-3 % on the
+// uniform graph and 2 % on the locality variant; adding non-temporal source
+// loads matches that on the uniform graph but costs 10 % on the locality
+// variant (its rows do reuse the cache), so the default is stores only.
+// Other widths fall back to Vec.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <typename T, int V, bool NT>
 __device__ __forceinline__ void load_vec(const T* p, float* r) {
@@ -139,13 +140,15 @@ __device__ __forceinline__ void store_vec(T* p, const float* r) {
 }
 // Gathers switch to non-temporal access when the gathered table (estimated as
 // rows x leading dimension: the graphs here are square) reaches this size.
-// SLDM_GATHER_NT=0 / =1 in the environment forces it off / on (read per call).
+// Mode bits: 1 = output stores, 2 = source-row loads.  SLDM_GATHER_NT in the
+// environment forces a mode: 0 none, s stores only, 1 both (read per call).
 constexpr int64_t kNtTableBytes = (int64_t)1 << 30;
-inline bool nt_gather(int64_t table_bytes) {
+inline int nt_gather(int64_t table_bytes) {
   const char* e = getenv("SLDM_GATHER_NT");
-  if (e && e[0] == '0') return false;
-  if (e && e[0] == '1') return true;
-  return table_bytes >= kNtTableBytes;
+  if (e && e[0] == '0') return 0;
+  if (e && e[0] == 's') return 1;
+  if (e && e[0] == '1') return 3;
+  return table_bytes >= kNtTableBytes ? 1 : 0;
 }
 
 // Widest element count V (16 B max per lane) such that feat, the leading

@@ -17,8 +17,8 @@
 //   - up to 8 source rows per row-group are in flight before the first
 //     accumulate (batches of 8/4/2/1, no per-element predication, so the
 //     compiler keeps the loads un-waited);
-//   - tables >= 1 GiB: source rows loaded and output rows stored non-temporal
-//     (sldm::load_vec / store_vec; +6-8 % at C4);
+//   - tables >= 1 GiB: output rows stored non-temporal (sldm::store_vec,
+//     nt_gather in common.hpp; source-row loads stay cached);
 //   - fp32 accumulation in CSR order -> bit-identical to the reference's CPU
 //     scatter_add_ for fp32 input; the mean divides by the fp32 degree
 //     (PyG divides by the fp32 count).
@@ -28,7 +28,7 @@ namespace {
 
 constexpr int kBlock = 256;
 
-template <typename TI, typename TO, int V, int NCH, bool MEAN, bool ADD, bool NT>
+template <typename TI, typename TO, int V, int NCH, bool MEAN, bool ADD, int NT>
 __global__ __launch_bounds__(kBlock) void gather_rows_kernel(
     const TI* __restrict__ x, int64_t ldx, const int32_t* __restrict__ rowptr,
     const int32_t* __restrict__ col, const int32_t* __restrict__ order, int64_t nrows,
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int c = 0; c < NCH; ++c)
-        sldm::load_vec<TI, V, NT>(x + (int64_t)idx[u] * ldx + f0[c], d[u][c]);
+        sldm::load_vec<TI, V, (NT & 2) != 0>(x + (int64_t)idx[u] * ldx + f0[c], d[u][c]);
     return [&, d]() mutable {
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(
 #pragma unroll
       for (int v = 0; v < V; ++v) acc[c][v] = a[c][v] + acc[c][v];
     }
-    sldm::store_vec<TO, V, NT>(out + row * ldo + f0[c], acc[c]);
+    sldm::store_vec<TO, V, (NT & 1) != 0>(out + row * ldo + f0[c], acc[c]);
   }
 }
 
@@ -139,15 +139,15 @@ int launch_nch(const TI* x, int64_t ldx, const int32_t* rowptr, const int32_t* c
   const int64_t threads = nrows << lpr_log2;
   const int64_t grid = (threads + kBlock - 1) / kBlock;
   SLDM_REQUIRE(grid < ((int64_t)1 << 31), "sldm_gather_rows: grid too large");
-  const bool nt = sldm::nt_gather(nrows * ldx * (int64_t)sizeof(TI));
+  const int nt = sldm::nt_gather(nrows * ldx * (int64_t)sizeof(TI));
+#define SLDM_GATHER_LAUNCH(NC, NTV)                                                           \
+  gather_rows_kernel<TI, TO, V, NC, MEAN, ADD, NTV><<<(unsigned)grid, kBlock, 0, stream>>>(  \
+      x, ldx, rowptr, col, order, nrows, feat, lpr_log2, addend, lda, out, ldo)
 #define SLDM_GATHER_CASE(NC)                                                                 \
   case NC:                                                                                   \
-    if (nt)                                                                                  \
-      gather_rows_kernel<TI, TO, V, NC, MEAN, ADD, true><<<(unsigned)grid, kBlock, 0, stream>>>( \
-          x, ldx, rowptr, col, order, nrows, feat, lpr_log2, addend, lda, out, ldo);         \
-    else                                                                                     \
-      gather_rows_kernel<TI, TO, V, NC, MEAN, ADD, false><<<(unsigned)grid, kBlock, 0, stream>>>( \
-          x, ldx, rowptr, col, order, nrows, feat, lpr_log2, addend, lda, out, ldo);         \
+    if (nt == 3) SLDM_GATHER_LAUNCH(NC, 3);                                                  \
+    else if (nt == 1) SLDM_GATHER_LAUNCH(NC, 1);                                             \
+    else SLDM_GATHER_LAUNCH(NC, 0);                                                          \
     break;
   switch (nch) {
     SLDM_GATHER_CASE(1)
@@ -159,6 +159,7 @@ int launch_nch(const TI* x, int64_t ldx, const int32_t* rowptr, const int32_t* c
       return SLDM_ERR_ARG;
   }
 #undef SLDM_GATHER_CASE
+#undef SLDM_GATHER_LAUNCH
   SLDM_LAUNCH_CHECK("gather_rows_kernel");
   return SLDM_OK;
 }

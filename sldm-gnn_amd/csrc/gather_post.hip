@@ -26,7 +26,7 @@ namespace {
 
 constexpr int kBlock = 256;
 
-template <typename T, int V, int NCH, bool NT>
+template <typename T, int V, int NCH, int NT>
 __global__ __launch_bounds__(kBlock) void gather_post_bwd_kernel(
     const T* __restrict__ g, int64_t ldg, const int32_t* __restrict__ t_rowptr,
     const int32_t* __restrict__ t_col, const int32_t* __restrict__ order,
@@ -113,7 +113,7 @@ __global__ __launch_bounds__(kBlock) void gather_post_bwd_kernel(
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int c = 0; c < NCH; ++c)
-          sldm::load_vec<T, V, NT>(g + (int64_t)idx[u] * ldg + f0[c], d[u][c]);
+          sldm::load_vec<T, V, (NT & 2) != 0>(g + (int64_t)idx[u] * ldg + f0[c], d[u][c]);
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(kBlock) void gather_post_bwd_kernel(
         mine[feat + f0[c] + v] += dy[c][v];
         mine[2 * feat + f0[c] + v] += o[v];
       }
-      sldm::store_vec<T, V, NT>(dh + row * (int64_t)feat + f0[c], o);
+      sldm::store_vec<T, V, (NT & 1) != 0>(dh + row * (int64_t)feat + f0[c], o);
     }
   }
 
@@ -191,8 +191,8 @@ int launch_v(int nch, int lpr_log2, int np, const void* g, int64_t ldg, const in
              void* dh, float* partials, hipStream_t stream) {
   const size_t lds = sizeof(float) * (size_t)feat * (3 * (kBlock >> lpr_log2) + 2);
   SLDM_REQUIRE(lds <= 160 * 1024, "sldm_gather_post_bwd: feat=%d needs %zu B of LDS", feat, lds);
-  // non-temporal gathered rows and dh stores on GiB-scale tables (common.hpp)
-  const bool nt = sldm::nt_gather(nrows * ldg * (int64_t)sizeof(T));
+  // non-temporal dh stores on GiB-scale tables (common.hpp nt_gather)
+  const int nt = sldm::nt_gather(nrows * ldg * (int64_t)sizeof(T));
 #define SLDM_GPB_LAUNCH(NC, NTV)                                                               \
   gather_post_bwd_kernel<T, V, NC, NTV><<<np, kBlock, lds, stream>>>(                          \
       (const T*)g, ldg, t_rowptr, t_col, order, (const T*)addend, lda, nrows, feat,            \
@@ -200,7 +200,9 @@ int launch_v(int nch, int lpr_log2, int np, const void* g, int64_t ldg, const in
       partials)
 #define SLDM_GPB_CASE(NC)                                                                      \
   case NC:                                                                                     \
-    if (nt) SLDM_GPB_LAUNCH(NC, true); else SLDM_GPB_LAUNCH(NC, false);                        \
+    if (nt == 3) SLDM_GPB_LAUNCH(NC, 3);                                                       \
+    else if (nt == 1) SLDM_GPB_LAUNCH(NC, 1);                                                  \
+    else SLDM_GPB_LAUNCH(NC, 0);                                                               \
     break;
   switch (nch) {
     SLDM_GPB_CASE(1)

@@ -84,7 +84,9 @@ def main() -> None:
            "correction": "hbm_read_bytes = 2 * FETCH_SIZE * 1024 (gfx950), "
                          "hbm_write_bytes = WRITE_SIZE * 1024",
            "kernels": kernels}
-    gk = [k for k in kernels if k.startswith("gather_rows_kernel") and "true, false>" in k]
+    # the forward mean gather: <TI, TO, V, NCH, MEAN=true, ADD=false[, NT]>
+    gk = [k for k in kernels if k.startswith("gather_rows_kernel")
+          and ("true, false>" in k or "true, false, true>" in k or "true, false, false>" in k)]
     if gk and a.gather_alg_bytes:
         res["gather_fwd_c4"] = {"kernel": gk[0],
                                 "hbm_bytes_per_launch": kernels[gk[0]]["hbm_bytes_per_launch_first"],
