@@ -18,6 +18,7 @@ import csv
 import glob
 import json
 import os
+import re
 from collections import defaultdict
 
 
@@ -86,7 +87,7 @@ def main() -> None:
            "kernels": kernels}
     # the forward mean gather: <TI, TO, V, NCH, MEAN=true, ADD=false[, NT]>
     gk = [k for k in kernels if k.startswith("gather_rows_kernel")
-          and ("true, false>" in k or "true, false, true>" in k or "true, false, false>" in k)]
+          and re.search(r"true, false(, \w+)?>$", k)]
     if gk and a.gather_alg_bytes:
         res["gather_fwd_c4"] = {"kernel": gk[0],
                                 "hbm_bytes_per_launch": kernels[gk[0]]["hbm_bytes_per_launch_first"],
