@@ -781,6 +781,40 @@ def test_gather_post_bwd_equals_gather_then_post(dtype, n, e, f, drop):
         torch.testing.assert_close(a, b, atol=1e-3, rtol=1e-4)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gather_cache_policy_modes_bit_equal(dtype, monkeypatch):
+    """SLDM_GATHER_NT forces the gathers' cache-policy mode (0: cached, s:
+    non-temporal output stores -- the default on GiB tables --, 1: non-temporal
+    loads and stores); the hint changes no arithmetic: forward mean gather,
+    transpose gather with addend and the fused boundary kernel are bit-equal
+    across modes."""
+    from sldm_sage import build_graph, ops
+    n, e, f = 4001, 30000, 256
+    ei, _ = _graph(n, e, 1, seed=3)
+    gr = build_graph(ei.to(DEV), n)
+    gen = torch.Generator(device=DEV).manual_seed(9)
+    x, g, addend, xhat = (torch.randn(n, f, generator=gen, device=DEV).to(dtype)
+                          for _ in range(4))
+    rstd = torch.rand(n, generator=gen, device=DEV) + 0.5
+    gamma = torch.randn(f, generator=gen, device=DEV)
+    beta = torch.randn(f, generator=gen, device=DEV) * 0.1
+
+    def run(mode):
+        monkeypatch.setenv("SLDM_GATHER_NT", mode)
+        fwd = ops.gather_rows(x, gr.rowptr, gr.col, n, mean=True)
+        bwd = ops.gather_rows(g, gr.t_rowptr, gr.t_col, n, mean=False, addend=addend,
+                              order=gr.t_order)
+        fused = ops.gather_post_bwd(g, gr.t_rowptr, gr.t_col, gr.t_order, addend, xhat, rstd,
+                                    gamma, beta, 0.1, 0.25, 77)
+        torch.cuda.synchronize()
+        return [fwd, bwd, *fused]
+
+    base = run("0")
+    for mode in ("s", "1"):
+        for a, b in zip(run(mode), base):
+            assert torch.equal(a, b), mode
+
+
 @pytest.mark.parametrize("hd", [[256, 256, 256], [32, 64, 64]])
 def test_side_stream_weight_grads_bit_equal(hd, monkeypatch):
     """SLDM_OVERLAP_DW (weight gradients on a side stream) changes only where
