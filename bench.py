@@ -272,8 +272,9 @@ def main():
         step_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)]
         ops.set_timing_hook(None)
         if world > 1:
+            from sldm_sage.dist import all_reduce
             tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-            torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+            all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
             elapsed = tt.item()
 
         # CSR-build-inclusive step (N=1: static-graph cache cleared once)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SLDM_ABI_VERSION 2
+#define SLDM_ABI_VERSION 3
 
 enum sldm_dtype { SLDM_F32 = 0, SLDM_BF16 = 1 };
 enum sldm_status { SLDM_OK = 0, SLDM_ERR_ARG = 1, SLDM_ERR_HIP = 2 };
@@ -82,6 +82,28 @@ int sldm_gather_rows(int x_dtype, const void* x, int64_t ldx,
                      int64_t num_rows, int64_t feat, int mean,
                      const void* addend, int64_t ld_add,
                      int out_dtype, void* out, int64_t ldo, void* stream);
+
+/* sldm_gather_rows with high-degree rows split (BASELINE C5: power-law
+ * in-degrees up to ~10^4).  Rows with degree > max_deg
+ * ("hubs", listed in hub_rows) are summed as fixed-length edge chunks:
+ * chunk c covers CSR positions [chunk_beg[c], min(chunk_beg[c] + chunk_len,
+ * rowptr[chunk_row[c]+1])) and is summed by its own row group into the fp32
+ * row partials[c, 0:feat] (chunks of hub h are hub_chunk_ptr[h] ..
+ * hub_chunk_ptr[h+1]-1, in CSR order); a second pass adds hub h's partials
+ * in chunk order, then divides / adds the addend / stores like any row.
+ * Every other row (all rows, or row_order's) is summed as in
+ * sldm_gather_rows.  Deterministic; hub rows equal the CPU's sequential
+ * order up to fp32 reassociation at chunk boundaries.  partials: num_chunks
+ * x feat fp32 scratch.  Same dtype / addend / row_order contract as
+ * sldm_gather_rows. */
+int sldm_gather_rows_split(int x_dtype, const void* x, int64_t ldx,
+                           const int32_t* rowptr, const int32_t* col, const int32_t* row_order,
+                           int64_t num_rows, int64_t feat, int mean,
+                           const void* addend, int64_t ld_add, int out_dtype, void* out,
+                           int64_t ldo, const int32_t* hub_rows, const int32_t* hub_chunk_ptr,
+                           int64_t num_hubs, const int32_t* chunk_row, const int32_t* chunk_beg,
+                           int64_t num_chunks, int32_t chunk_len, int32_t max_deg,
+                           float* partials, void* stream);
 
 /* g[i,:] = d[i,:] / max(1, rowptr[i+1]-rowptr[i]), in place, dtype of d.
  * Backward of the mean's division (A8) folded before the transpose sum. */

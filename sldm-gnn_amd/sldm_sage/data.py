@@ -24,6 +24,7 @@ dataset.py:85):
 """
 from __future__ import annotations
 
+import weakref
 from collections.abc import Mapping
 
 import numpy as np
@@ -76,13 +77,26 @@ def host_csr(edge_index: torch.Tensor, num_nodes: int):
 
 
 def graph_csr(data, edge_index: torch.Tensor, num_nodes: int):
-    """The graph's host CSR pair, cached on the graph object when possible."""
+    """The graph's host CSR pair, cached on the graph object when possible.
+
+    The entry is keyed on the edge_index tensor itself -- a weak reference
+    plus its ``_version`` counter, as the SageBlock's graph cache does -- so a
+    replaced edge_index, or one edited in place (augmentation, rewiring),
+    is rebuilt even when its edge count is unchanged."""
     cached = getattr(data, _CSR_ATTR, None) if not isinstance(data, Mapping) else \
         data.get(_CSR_ATTR)
-    if cached is not None and cached[0] == num_nodes and cached[1] == int(edge_index.size(1)):
-        return cached[2]
+    versioned = not edge_index.is_inference()
+    if (cached is not None and versioned and cached[0] == num_nodes
+            and cached[1]() is edge_index and cached[2] == edge_index._version):
+        return cached[3]
     csr = host_csr(edge_index, num_nodes)
-    entry = (num_nodes, int(edge_index.size(1)), csr)
+    if not versioned:           # inference tensors carry no version counter
+        return csr
+    try:
+        ref = weakref.ref(edge_index)
+    except TypeError:
+        return csr
+    entry = (num_nodes, ref, edge_index._version, csr)
     try:
         if isinstance(data, Mapping):
             data[_CSR_ATTR] = entry

@@ -144,14 +144,110 @@ class HipBackend:
         return out
 
 
+# ---------------------------------------------------------------------------
+# Collectives.  RCCL ("nccl") takes device tensors directly.  Under gloo (the
+# CPU tests, and several ranks sharing one GPU in a rehearsal) device tensors
+# are staged through host memory explicitly: ``.cpu()`` waits for the
+# producing HIP stream, the collective runs on host tensors, and the result is
+# copied back on the current stream.  Gloo's own CUDA path (its internal
+# streams and pinned staging buffers, raced against our kernels on the current
+# stream and the caching allocator) is never used.  Staged calls complete
+# synchronously and return ``None`` as their work handle.
+# ---------------------------------------------------------------------------
+def _host_staged(t: torch.Tensor, group) -> bool:
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group=None,
+                      async_op: bool = False):
+    """``dist.all_to_all_single`` with gloo host staging (module note above)."""
+    if _host_staged(out, group):
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(o, inp.cpu(), output_split_sizes=out_splits,
+                               input_split_sizes=in_splits, group=group)
+        out.copy_(o)
+        return None
+    return dist.all_to_all_single(out, inp, output_split_sizes=out_splits,
+                                  input_split_sizes=in_splits, group=group, async_op=async_op)
+
+
+def all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None, async_op: bool = False):
+    """In-place ``dist.all_reduce`` with gloo host staging."""
+    if _host_staged(t, group):
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+        return None
+    return dist.all_reduce(t, op=op, group=group, async_op=async_op)
+
+
+def broadcast(t: torch.Tensor, src: int = 0, group=None) -> None:
+    """In-place ``dist.broadcast`` with gloo host staging."""
+    if _host_staged(t, group):
+        h = t.cpu()
+        dist.broadcast(h, src=src, group=group)
+        t.copy_(h)
+        return
+    dist.broadcast(t, src=src, group=group)
+
+
+# ---------------------------------------------------------------------------
+# Row blocks.  Rank r owns the contiguous node rows [bounds[r], bounds[r+1]).
+# "rows": equal row counts (P = ceil(N/W)); "cost": cut by the cumulative
+# per-node cost (in-degree + out-degree + the dense part's row cost in
+# edge-equivalents), SURVEY.md §8e's "split by cumulative in-degree" for
+# power-law graphs -- a 10k-in-degree hub then weighs as much as ~10k rows'
+# edges instead of one row.
+# ---------------------------------------------------------------------------
+# dense part per row (13 F s bytes at ~4 TB/s) vs one gathered edge (F s + 4
+# bytes at ~5.3 TB/s): ~17 edge-equivalents per row (two gathers per layer).
+_ROW_COST_EDGES = 17.0
+
+
+def row_bounds(edge_index: torch.Tensor, num_nodes: int, world: int,
+               balance: str = "cost") -> list[int]:
+    """[W+1] row offsets of the W contiguous row blocks (same on every rank:
+    edge_index is the same everywhere).  ``balance`` = "rows" or "cost"."""
+    if balance == "rows" or world == 1 or num_nodes == 0:
+        P = (num_nodes + world - 1) // world
+        return [min(r * P, num_nodes) for r in range(world + 1)]
+    if balance != "cost":
+        raise ValueError(f"unknown balance {balance!r} (rows, cost)")
+    dev = edge_index.device
+    w = torch.full((num_nodes,), _ROW_COST_EDGES, dtype=torch.float64, device=dev)
+    if edge_index.numel():
+        ones = torch.ones(edge_index.size(1), dtype=torch.float64, device=dev)
+        w.index_add_(0, edge_index[1].long(), ones)
+        w.index_add_(0, edge_index[0].long(), ones)
+    cum = torch.cumsum(w, 0)
+    total = float(cum[-1])
+    targets = torch.tensor([total * r / world for r in range(1, world)], dtype=torch.float64,
+                           device=dev)
+    cuts = torch.searchsorted(cum, targets).tolist() if world > 1 else []
+    bounds = [0] + [min(int(c) + 1, num_nodes) for c in cuts] + [num_nodes]
+    for r in range(1, world + 1):        # monotone (empty blocks allowed)
+        bounds[r] = max(bounds[r], bounds[r - 1])
+    return bounds
+
+
+def _owner(ids: torch.Tensor, bounds: list[int]) -> torch.Tensor:
+    b = torch.tensor(bounds[1:-1], dtype=ids.dtype, device=ids.device)
+    return torch.searchsorted(b, ids, right=True)
+
+
 @dataclass
 class HaloPlan:
-    """Which own rows go to which peer, and how many rows come back."""
+    """Which own rows go to which peer, and how many rows come back.
+
+    ``active`` is global: whether ANY rank sends or receives anything in this
+    exchange (all ranks agree, so they all issue the collective or all skip
+    it -- a locally decided skip would desynchronise the process group)."""
 
     send_idx: torch.Tensor        # local row ids, grouped by destination peer
     send_rowptr: torch.Tensor     # identity CSR (arange) for the pack gather
     send_counts: list[int]
     recv_counts: list[int]
+    active: bool = True
 
     @property
     def num_recv(self) -> int:
@@ -202,7 +298,7 @@ class GraphPartition:
     rank: int
     world: int
     num_nodes: int
-    rows_per_rank: int           # P
+    bounds: list[int]            # [W+1] row-block offsets (row_bounds)
     row_begin: int
     row_end: int
     fwd: SageGraph               # rows = own nodes, col = halo-buffer positions (sources)
@@ -231,28 +327,32 @@ def _exchange_counts(counts: list[int], device, group) -> list[int]:
         return list(counts)
     send = torch.tensor(counts, dtype=torch.int64, device=device)
     recv = torch.empty_like(send)
-    dist.all_to_all_single(recv, send, group=group)
+    all_to_all_single(recv, send, None, None, group=group)
     return recv.tolist()
 
 
-def _build_plan(ids: torch.Tensor, r0: int, r1: int, P: int, world: int, group):
+def _build_plan(ids: torch.Tensor, r0: int, r1: int, bounds: list[int], world: int, group):
     """ids: global node ids this rank references (any order, duplicates ok).
 
     Returns (remap, plan): remap(global ids) -> halo-buffer positions."""
     dev = ids.device
     uniq = torch.unique(ids)                                   # sorted
     remote = uniq[(uniq < r0) | (uniq >= r1)]                  # sorted => grouped by owner
-    owner = torch.div(remote, P, rounding_mode="floor")
+    owner = _owner(remote, bounds)
     need_counts = torch.bincount(owner, minlength=world)[:world].tolist()
     give_counts = _exchange_counts(need_counts, dev, group)
     # tell each owner which of its rows we need (global ids), learn what to send
     if world > 1:
         wanted = torch.empty(sum(give_counts), dtype=torch.int64, device=dev)
-        dist.all_to_all_single(wanted, remote.to(torch.int64).contiguous(),
-                               output_split_sizes=give_counts,
-                               input_split_sizes=need_counts, group=group)
+        all_to_all_single(wanted, remote.to(torch.int64).contiguous(), give_counts,
+                          need_counts, group=group)
+        # global decision: does any rank move anything in this exchange?
+        tot = torch.tensor([sum(need_counts) + sum(give_counts)], dtype=torch.int64, device=dev)
+        all_reduce(tot, group=group)
+        active = int(tot.item()) > 0
     else:
         wanted = remote.to(torch.int64)
+        active = False
     send_idx = (wanted - r0).to(torch.int32)
     n_own = r1 - r0
 
@@ -262,21 +362,23 @@ def _build_plan(ids: torch.Tensor, r0: int, r1: int, P: int, world: int, group):
         return torch.where(own, g - r0, n_own + pos).to(torch.int32)
 
     rowptr = torch.arange(send_idx.numel() + 1, dtype=torch.int32, device=dev)
-    return remap, HaloPlan(send_idx, rowptr, give_counts, need_counts)
+    return remap, HaloPlan(send_idx, rowptr, give_counts, need_counts, active)
 
 
 def partition_graph(edge_index: torch.Tensor, num_nodes: int, world: int, rank: int,
-                    backend=HipBackend, group=None) -> GraphPartition:
+                    backend=HipBackend, group=None, balance: str = "cost") -> GraphPartition:
     """Build rank ``rank``'s partition from the full edge_index (same on every
-    rank).  Collective over ``group`` (the halo lists are exchanged here)."""
-    P = (num_nodes + world - 1) // world
-    r0, r1 = min(rank * P, num_nodes), min((rank + 1) * P, num_nodes)
+    rank).  Collective over ``group`` (the halo lists are exchanged here).
+    ``balance``: row blocks of equal size ("rows") or of equal modelled cost
+    ("cost", :func:`row_bounds`)."""
+    bounds = row_bounds(edge_index, num_nodes, world, balance)
+    r0, r1 = bounds[rank], bounds[rank + 1]
     n = r1 - r0
     src, dst = edge_index[0], edge_index[1]
     ein = edge_index[:, (dst >= r0) & (dst < r1)]     # original order kept
     eout = edge_index[:, (src >= r0) & (src < r1)]
-    remap_f, plan_f = _build_plan(ein[0], r0, r1, P, world, group)
-    remap_b, plan_b = _build_plan(eout[1], r0, r1, P, world, group)
+    remap_f, plan_f = _build_plan(ein[0], r0, r1, bounds, world, group)
+    remap_b, plan_b = _build_plan(eout[1], r0, r1, bounds, world, group)
     n_buf_f = n + plan_f.num_recv
     n_buf_b = n + plan_b.num_recv
     # CSR by (local) destination over buffer-position sources, and by (local)
@@ -287,7 +389,7 @@ def partition_graph(edge_index: torch.Tensor, num_nodes: int, world: int, rank: 
     _, _, trp, tcol = backend.csr(fout, max(n_buf_b, 1), True)
     fwd = SageGraph(n, int(ein.size(1)), rp[: n + 1], col, None, None)
     bwd = SageGraph(n, int(eout.size(1)), trp[: n + 1], tcol, None, None)
-    return GraphPartition(rank, world, num_nodes, P, r0, r1, fwd, bwd, plan_f, plan_b,
+    return GraphPartition(rank, world, num_nodes, bounds, r0, r1, fwd, bwd, plan_f, plan_b,
                           _split_rows(fwd, n), _split_rows(bwd, n))
 
 
@@ -312,18 +414,34 @@ def _halo_buffer(x_own: torch.Tensor, plan: HaloPlan, backend, group, async_op=F
     With ``async_op`` returns (buf, work): the exchange runs on RCCL's stream
     while the caller queues independent kernels; ``work.wait()`` before use."""
     n, F = x_own.shape
-    if plan.num_recv == 0 and sum(plan.send_counts) == 0:
-        return (x_own, None) if async_op else x_own   # nothing crosses: no copy
+    if not plan.active:
+        # no rank moves anything (decided globally at partition time): every
+        # rank skips the collective together
+        return (x_own, None) if async_op else x_own
     buf = x_own.new_empty(n + plan.num_recv, F)
     buf[:n].copy_(x_own)
-    work = None
-    if plan.num_recv or sum(plan.send_counts):
-        send = (backend.pick_rows(x_own, plan.send_rowptr, plan.send_idx)
-                if plan.send_idx.numel() else x_own.new_empty(0, F))
-        work = dist.all_to_all_single(buf[n:], send, output_split_sizes=plan.recv_counts,
-                                      input_split_sizes=plan.send_counts, group=group,
-                                      async_op=async_op)
+    send = (backend.pick_rows(x_own, plan.send_rowptr, plan.send_idx)
+            if plan.send_idx.numel() else x_own.new_empty(0, F))
+    work = all_to_all_single(buf[n:], send, plan.recv_counts, plan.send_counts, group=group,
+                             async_op=async_op)
+    if work is not None and async_op:
+        # the caching allocator may hand `send`'s block to the next allocation
+        # on this stream; keep it alive until the caller waits
+        work = _KeepAlive(work, send)
     return (buf, work) if async_op else buf
+
+
+class _KeepAlive:
+    """A collective's work handle that also holds its input buffer."""
+
+    __slots__ = ("work", "keep")
+
+    def __init__(self, work, keep):
+        self.work, self.keep = work, keep
+
+    def wait(self):
+        self.work.wait()
+        self.keep = None
 
 
 # ---------------------------------------------------------------------------
@@ -430,8 +548,7 @@ def partition_features(edge_index: torch.Tensor, num_nodes: int, world: int, ran
 
 
 def _a2a(out, inp, out_splits, in_splits, group):
-    return dist.all_to_all_single(out, inp, output_split_sizes=out_splits,
-                                  input_split_sizes=in_splits, group=group, async_op=True)
+    return all_to_all_single(out, inp, out_splits, in_splits, group=group, async_op=True)
 
 
 def _rows_to_cols(part: FeaturePartition, src: torch.Tensor, j: int, dst_cols: torch.Tensor,
@@ -617,7 +734,7 @@ class _FeatLayerFn(torch.autograd.Function):
         flat = torch.cat([t.reshape(-1).float() for t in grads])
         rwork = None
         if part.world > 1:
-            rwork = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group, async_op=True)
+            rwork = all_reduce(flat, op=dist.ReduceOp.SUM, group=group, async_op=True)
         _wait_all(works)
         # dx = dx_root + the gathered gradient, added as the blocks are unpacked
         dx = _feat_aggregate_to_rows(be, part, g_cols, gr.t_rowptr, gr.t_col, False, F,
@@ -666,7 +783,7 @@ class _DistLayerFn(torch.autograd.Function):
         flat = torch.cat([t.reshape(-1).float() for t in grads])
         rwork = None
         if part.world > 1:
-            rwork = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group, async_op=True)
+            rwork = all_reduce(flat, op=dist.ReduceOp.SUM, group=group, async_op=True)
         dx = _overlapped_gather(be, buf, xwork, part.bwd, part.bwd_split, part.num_rows, False,
                                 addend=dx_r.contiguous())
         if rwork is not None:
@@ -697,7 +814,7 @@ class DistSageBlock(nn.Module):
         if broadcast_params and partition.world > 1:
             with torch.no_grad():
                 for p in block.parameters():
-                    dist.broadcast(p.data, src=0, group=group)
+                    broadcast(p.data, src=0, group=group)
 
     @property
     def strategy(self) -> str:
@@ -718,7 +835,7 @@ class DistSageBlock(nn.Module):
         for i, (conv, post) in enumerate(layers):
             ln, act, drop = post[0], post[1], post[2]
             p = _drop_p(drop)
-            seed = _new_seed() if p > 0 else 0
+            seed = _new_seed(x.device) if p > 0 else 0
             args = (x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, ln.weight, ln.bias,
                     self.part, self.group, self.backend, _act_slope(act), p, seed, float(ln.eps))
             if feat:
@@ -780,19 +897,22 @@ def estimate_strategies(edge_index: torch.Tensor, num_nodes: int, world: int, ra
     strategies: exchange bytes / xGMI + gather bytes / measured gather rate +
     dense bytes / stream rate, max over ranks (collective over ``group`` when
     world > 1, so every rank gets the same numbers)."""
-    P = (num_nodes + world - 1) // world
-    r0, r1 = min(rank * P, num_nodes), min((rank + 1) * P, num_nodes)
+    hb_ = row_bounds(edge_index, num_nodes, world, "cost")     # partition_graph's blocks
+    h0, h1 = hb_[rank], hb_[rank + 1]
     src, dst = edge_index[0], edge_index[1]
-    in_mask = (dst >= r0) & (dst < r1)
-    out_mask = (src >= r0) & (src < r1)
-    halo_f = _remote_unique(src[in_mask], r0, r1)
-    halo_b = _remote_unique(dst[out_mask], r0, r1)
+    in_mask = (dst >= h0) & (dst < h1)
+    out_mask = (src >= h0) & (src < h1)
+    halo_f = _remote_unique(src[in_mask], h0, h1)
+    halo_b = _remote_unique(dst[out_mask], h0, h1)
     e_in, e_out = int(in_mask.sum()), int(out_mask.sum())
     link = max(world - 1, 1) * _LINK_BPS
     row = feat * elem
-    dense_own = _DENSE_BYTES_PER_ROW_FS * (r1 - r0) * row / _DENSE_BPS
     halo_t = ((halo_f + halo_b) * row / link
-              + (e_in + e_out) * (row + 4) / _gather_rate(row) + dense_own)
+              + (e_in + e_out) * (row + 4) / _gather_rate(row)
+              + _DENSE_BYTES_PER_ROW_FS * (h1 - h0) * row / _DENSE_BPS)
+    P = (num_nodes + world - 1) // world                       # partition_features' blocks
+    r0, r1 = min(rank * P, num_nodes), min((rank + 1) * P, num_nodes)
+    dense_own = _DENSE_BYTES_PER_ROW_FS * (r1 - r0) * row / _DENSE_BPS
     fc = max(1, feat // world)
     e = int(edge_index.size(1))
     # feature slicing pipelines its switches over `chunks` row chunks: the
@@ -807,7 +927,7 @@ def estimate_strategies(edge_index: torch.Tensor, num_nodes: int, world: int, ra
     v = torch.tensor([halo_t, feat_t, rep_t, float(halo_f), float(halo_b)], dtype=torch.float64,
                      device=edge_index.device)
     if world > 1:
-        dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
+        all_reduce(v, op=dist.ReduceOp.MAX, group=group)
     halo_t, feat_t, rep_t, hf, hb = v.tolist()
     return {"halo_s": halo_t, "feature_s": feat_t, "replicate_s": rep_t,
             "halo_rows_fwd_max": int(hf), "halo_rows_bwd_max": int(hb)}
@@ -851,7 +971,7 @@ def partition_replicated(edge_index: torch.Tensor, num_nodes: int, world: int, r
 
 def plan_partition(edge_index: torch.Tensor, num_nodes: int, world: int, rank: int,
                    feat: int, elem: int, strategy: str = "auto", backend=HipBackend,
-                   group=None, chunks: int = 4):
+                   group=None, chunks: int = 4, balance: str = "cost"):
     """Partition with ``strategy`` in {"auto", "halo", "feature", "replicate"};
     "auto" takes :func:`choose_strategy` of :func:`estimate_strategies`
     (every rank gets the same answer: the estimate is max-reduced).  Returns
@@ -870,6 +990,7 @@ def plan_partition(edge_index: torch.Tensor, num_nodes: int, world: int, rank: i
     if strategy == "replicate":
         return partition_replicated(edge_index, num_nodes, world, rank, backend), info
     if strategy == "halo":
-        return partition_graph(edge_index, num_nodes, world, rank, backend, group), info
+        return partition_graph(edge_index, num_nodes, world, rank, backend, group,
+                               balance), info
     raise ValueError(f"unknown partition strategy {strategy!r} "
                      "(auto, halo, feature, replicate)")

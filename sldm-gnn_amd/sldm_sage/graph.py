@@ -22,6 +22,23 @@ from . import ops
 
 
 @dataclass
+class HubPlan:
+    """High-degree rows of one CSR, split into fixed-length edge chunks for
+    ``sldm_gather_rows_split`` (include/sldm_sage.h): rows with degree >
+    ``max_deg`` are summed chunk by chunk by separate row groups (fp32
+    partials, combined in chunk order) instead of serially by one."""
+
+    hub_rows: torch.Tensor          # int32 [H]
+    chunk_ptr: torch.Tensor         # int32 [H+1]: chunks of hub h
+    chunk_row: torch.Tensor         # int32 [C]
+    chunk_beg: torch.Tensor         # int32 [C]: first CSR position of chunk c
+    num_hubs: int
+    num_chunks: int
+    chunk_len: int
+    max_deg: int
+
+
+@dataclass
 class SageGraph:
     """CSR of one graph on one device (int32)."""
 
@@ -31,8 +48,10 @@ class SageGraph:
     col: torch.Tensor               # [E]   sources, original edge order per row
     t_rowptr: torch.Tensor | None   # [N+1] by source (backward)
     t_col: torch.Tensor | None      # [E]   destinations
-    order: torch.Tensor | None = None     # longest-first schedule of rowptr rows (skewed graphs)
+    order: torch.Tensor | None = None     # longest-first schedule of rowptr rows (SLDM_SKEW=order)
     t_order: torch.Tensor | None = None   # same for t_rowptr
+    hub: HubPlan | None = None            # high-degree split of rowptr rows (skewed graphs)
+    t_hub: HubPlan | None = None          # same for t_rowptr
 
     @property
     def device(self) -> torch.device:
@@ -42,36 +61,85 @@ class SageGraph:
         return self.rowptr[1:] - self.rowptr[:-1]
 
 
+# Skew handling (power-law graphs).  Graphs below HUB_MIN_EDGES are
+# launch-bound (per-batch vehicle graphs: ~10^4 edges) and skip it -- and its
+# host sync -- entirely.  SLDM_SKEW: "split" (default: hub rows split into
+# chunks), "order" (round 1's longest-first schedule) or "none".
+HUB_MIN_EDGES = int(os.environ.get("SLDM_HUB_MIN_EDGES", str(1 << 20)))
+HUB_CHUNK = 256          # edges per hub chunk (one row group sums one chunk)
+
+
+def _skew_mode() -> str:
+    if os.environ.get("SLDM_NO_SCHEDULE") == "1":
+        return "none"
+    return os.environ.get("SLDM_SKEW", "split")
+
+
+def hub_threshold(num_nodes: int, num_edges: int) -> int:
+    """Rows with more in-edges than this are hubs: max(1024, 32 x mean degree)."""
+    return max(1024, int(32 * num_edges / max(num_nodes, 1)))
+
+
 def build_graph(edge_index: torch.Tensor, num_nodes: int, transpose: bool = True,
                 validate: bool = True) -> SageGraph:
     """Build the CSR pair on edge_index's device.
 
-    ``validate`` reads back the device-side range flag (one host sync) and
-    raises IndexError on a node id outside [0, num_nodes) — the reference
-    raises too (PyG index_select / scatter bounds checks).
+    ``validate`` reads back the device-side range flag and raises IndexError
+    on a node id outside [0, num_nodes) -- the reference raises too (PyG
+    index_select / scatter bounds checks).  That read is the build's only
+    host sync for graphs below HUB_MIN_EDGES; larger graphs read their
+    maximum degrees in the same sync (and a skewed one a second time, for
+    the hub plan's size).
     """
     rowptr, col, t_rowptr, t_col, bad = ops.csr_build(edge_index, num_nodes, transpose)
-    if validate and edge_index.size(1) > 0 and int(bad.item()) != 0:
+    E = int(edge_index.size(1))
+    g = SageGraph(num_nodes, E, rowptr, col, t_rowptr, t_col)
+    mode = _skew_mode()
+    skew_check = E >= HUB_MIN_EDGES and num_nodes > 0 and mode != "none"
+    if not (validate and E > 0) and not skew_check:
+        return g
+    stats = [bad.to(torch.int64).view(1)]
+    if skew_check:
+        stats.append((rowptr[1:] - rowptr[:-1]).max().to(torch.int64).view(1))
+        if t_rowptr is not None:
+            stats.append((t_rowptr[1:] - t_rowptr[:-1]).max().to(torch.int64).view(1))
+    vals = torch.cat(stats).tolist()                    # the one host sync
+    if validate and E > 0 and vals[0] != 0:
         raise IndexError(
             f"edge_index holds a node id outside [0, {num_nodes}) "
             "(the reference's index_select/scatter would raise as well)")
-    g = SageGraph(num_nodes, int(edge_index.size(1)), rowptr, col, t_rowptr, t_col)
-    g.order = _schedule(rowptr, g.num_edges)
-    if t_rowptr is not None:
-        g.t_order = _schedule(t_rowptr, g.num_edges)
+    if skew_check:
+        thr = hub_threshold(num_nodes, E)
+        if mode == "order":
+            if vals[1] > max(64, 8 * E / num_nodes):
+                g.order = ops.degree_order(rowptr)
+            if t_rowptr is not None and vals[2] > max(64, 8 * E / num_nodes):
+                g.t_order = ops.degree_order(t_rowptr)
+        else:
+            if vals[1] > thr:
+                g.hub = hub_plan(rowptr, thr)
+            if t_rowptr is not None and vals[2] > thr:
+                g.t_hub = hub_plan(t_rowptr, thr)
     return g
 
 
-def _schedule(rowptr: torch.Tensor, num_edges: int):
-    """Longest-first row order when the degree distribution is skewed
-    (max > max(64, 8 x mean)), e.g. power-law in-degrees; None otherwise."""
-    n = rowptr.numel() - 1
-    if n <= 0 or num_edges == 0 or os.environ.get("SLDM_NO_SCHEDULE") == "1":
+def hub_plan(rowptr: torch.Tensor, max_deg: int, chunk_len: int = HUB_CHUNK) -> HubPlan | None:
+    """Chunk table of the rows with degree > max_deg (None if there are none)."""
+    deg = (rowptr[1:] - rowptr[:-1]).long()
+    hubs = (deg > max_deg).nonzero().squeeze(1)
+    nch = (deg[hubs] + chunk_len - 1) // chunk_len
+    ptr = torch.zeros(hubs.numel() + 1, dtype=torch.int64, device=rowptr.device)
+    torch.cumsum(nch, 0, out=ptr[1:])
+    total = int(ptr[-1])                                # sync (hubs only)
+    if hubs.numel() == 0:
         return None
-    max_deg = int((rowptr[1:] - rowptr[:-1]).max().item())
-    if max_deg <= max(64, 8 * num_edges / n):
-        return None
-    return ops.degree_order(rowptr)
+    chunk_row = torch.repeat_interleave(hubs, nch, output_size=total)
+    local = (torch.arange(total, device=rowptr.device)
+             - torch.repeat_interleave(ptr[:-1], nch, output_size=total))
+    chunk_beg = rowptr.long()[chunk_row] + local * chunk_len
+    i32 = torch.int32
+    return HubPlan(hubs.to(i32), ptr.to(i32), chunk_row.to(i32), chunk_beg.to(i32),
+                   int(hubs.numel()), total, chunk_len, max_deg)
 
 
 class _GraphCache:

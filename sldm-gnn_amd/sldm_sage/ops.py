@@ -126,14 +126,19 @@ def degree_order(rowptr: torch.Tensor) -> torch.Tensor:
 def gather_rows(x: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor, num_rows: int,
                 mean: bool, addend: torch.Tensor | None = None,
                 out: torch.Tensor | None = None, name: str = "gather",
-                order: torch.Tensor | None = None, edges: int | None = None) -> torch.Tensor:
+                order: torch.Tensor | None = None, edges: int | None = None,
+                hub=None) -> torch.Tensor:
     """out[i] = (addend[i] +) sum_{k in row i} x[col[k]]  (/ max(1, deg_i) if mean).
 
     ``order`` (optional) lists the rows to compute, slot s -> row order[s]
     (``num_rows`` = len(order)): a schedule from :func:`degree_order`, or a
     row subset (then ``out`` holds all rows and ``edges`` is the subset's
-    edge count, for the timing hook's byte accounting)."""
+    edge count, for the timing hook's byte accounting).  ``hub`` (a
+    :class:`~sldm_sage.graph.HubPlan` of ``rowptr``): its high-degree rows
+    are summed as split edge chunks (``sldm_gather_rows_split``)."""
     dev = _require_gpu(x, rowptr, col, addend, out, order)
+    if hub is not None and order is not None:
+        raise ValueError("gather_rows: a hub plan covers all rows (no row order / subset)")
     if x.dim() != 2 or x.stride(1) != 1:
         x = x.contiguous()
     F = x.size(1)
@@ -147,6 +152,18 @@ def gather_rows(x: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor, num_ro
     E = col.numel()
     s = x.element_size()
     bytes_alg = (E if edges is None else edges) * (4 + F * s) + (num_rows + 1) * 4 + num_rows * F * s * (2 if addend is not None else 1)
+    if hub is not None:
+        partials = torch.empty(hub.num_chunks, F, dtype=torch.float32, device=dev)
+        with _Timed(name, bytes_alg):
+            _lib.check(_lib.load().sldm_gather_rows_split(
+                dtype_code(x), x.data_ptr(), x.stride(0), rowptr.data_ptr(),
+                col.data_ptr() if E else rowptr.data_ptr(), None, num_rows, F, int(bool(mean)),
+                _ptr(addend), addend.stride(0) if addend is not None else 0,
+                dtype_code(out), out.data_ptr(), out.stride(0), hub.hub_rows.data_ptr(),
+                hub.chunk_ptr.data_ptr(), hub.num_hubs, hub.chunk_row.data_ptr(),
+                hub.chunk_beg.data_ptr(), hub.num_chunks, hub.chunk_len, hub.max_deg,
+                partials.data_ptr(), _stream(dev)), "sldm_gather_rows_split")
+        return out
     with _Timed(name, bytes_alg):
         _lib.check(_lib.load().sldm_gather_rows(
             dtype_code(x), x.data_ptr(), x.stride(0), rowptr.data_ptr(),

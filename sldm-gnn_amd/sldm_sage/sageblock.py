@@ -46,10 +46,29 @@ def _drop_p(drop: nn.Module) -> float:
     raise TypeError(f"SageBlock post dropout must be Dropout or Identity, got {type(drop)}")
 
 
-def _new_seed() -> int:
-    # Drawn from torch's default CPU generator so torch.manual_seed governs it;
-    # no device sync.
-    return int(torch.randint(0, 2**62, (1,)).item())
+def _splitmix64(z: int) -> int:
+    z = (z + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return z ^ (z >> 31)
+
+
+_SEED_LOCK = __import__("threading").Lock()
+
+
+def _new_seed(device: torch.device | None = None) -> int:
+    """Dropout key of one layer call, drawn the way nn.Dropout on a GPU
+    draws its mask: from the device's default generator (its seed and philox
+    offset, the offset advanced per call), so torch.manual_seed governs the
+    masks and the caller's CPU RNG stream (DataLoader shuffling, CPU randn)
+    is left untouched.  No device sync."""
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    gen = torch.cuda.default_generators[dev.index if dev.index is not None
+                                        else torch.cuda.current_device()]
+    with _SEED_LOCK:
+        off = gen.get_offset()
+        gen.set_offset(off + 4)
+    return _splitmix64(gen.initial_seed() ^ _splitmix64(off)) & (2**62 - 1)
 
 
 class _SageLayerFn(torch.autograd.Function):
@@ -60,7 +79,7 @@ class _SageLayerFn(torch.autograd.Function):
                 seed: int, eps: float):
         n = x.size(0)
         agg = ops.gather_rows(x, graph.rowptr, graph.col, n, mean=True, name="gather_fwd",
-                              order=graph.order)
+                              order=graph.order, hub=graph.hub)
         needs_grad = any(ctx.needs_input_grad[:6])
         out, xhat, rstd = dense.sage_layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope,
                                                drop_p, seed, save=needs_grad)
@@ -90,7 +109,7 @@ class _SageLayerFn(torch.autograd.Function):
             # adds the root-path gradient as it sums over out-edges.
             g, dx_r = dense.sage_linear_bwd_data(dh, wl, wr, graph.rowptr)
             dx = ops.gather_rows(g, graph.t_rowptr, graph.t_col, x.size(0), mean=False,
-                                 order=graph.t_order,
+                                 order=graph.t_order, hub=graph.t_hub,
                                  addend=dx_r, name="gather_bwd")
         return (dx, dwl.to(wl.dtype), dbl.to(wl.dtype), dwr.to(wr.dtype),
                 dgamma.to(gamma.dtype), dbeta.to(beta.dtype), None, None, None, None, None)
@@ -134,7 +153,7 @@ class _SageStackFn(torch.autograd.Function):
         for i, (slope, drop_p, seed, eps) in enumerate(cfgs):
             wl, bl, wr, gamma, beta = params[5 * i: 5 * i + 5]
             agg = ops.gather_rows(h, graph.rowptr, graph.col, n, mean=True, name="gather_fwd",
-                                  order=graph.order)
+                                  order=graph.order, hub=graph.hub)
             out, xhat, rstd = dense.sage_layer_fwd(agg, h, wl, bl, wr, gamma, beta, eps, slope,
                                                    drop_p, seed, save=True)
             saved += [h, agg, xhat, rstd]
@@ -186,11 +205,20 @@ class _SageStackFn(torch.autograd.Function):
             g, dx_r = dense.sage_linear_bwd_data(dh, wl, wr, graph.rowptr)
             if i == 0:
                 dx = ops.gather_rows(g, graph.t_rowptr, graph.t_col, h.size(0), mean=False,
-                                     order=graph.t_order, addend=dx_r, name="gather_bwd")
+                                     order=graph.t_order, hub=graph.t_hub, addend=dx_r, name="gather_bwd")
                 break
             # boundary: layer i's input gradient straight into layer i-1's post backward
             slope, drop_p, seed, _ = cfgs[i - 1]
             gamma_b, beta_b = params[5 * (i - 1) + 3], params[5 * (i - 1) + 4]
+            if graph.t_hub is not None:
+                # out-degree hubs: the split transpose gather, then the post
+                # backward (the fused kernel sums each row in one row group)
+                dxi = ops.gather_rows(g, graph.t_rowptr, graph.t_col, h.size(0), mean=False,
+                                      hub=graph.t_hub, addend=dx_r, name="gather_bwd")
+                dh, dgamma, dbeta, dbl = ops.post_bwd(
+                    dxi, acts[4 * (i - 1) + 2], acts[4 * (i - 1) + 3], gamma_b, beta_b, slope,
+                    drop_p, seed, dh_dtype=x_in.dtype)
+                continue
             dh, dgamma, dbeta, dbl = ops.gather_post_bwd(
                 g, graph.t_rowptr, graph.t_col, graph.t_order, dx_r, acts[4 * (i - 1) + 2],
                 acts[4 * (i - 1) + 3], gamma_b, beta_b, slope, drop_p, seed)
@@ -238,7 +266,7 @@ class _MeanAggFn(torch.autograd.Function):
     def forward(ctx, x, graph: SageGraph):
         ctx.graph = graph
         ctx.n = x.size(0)
-        return ops.gather_rows(x, graph.rowptr, graph.col, x.size(0), mean=True, order=graph.order,
+        return ops.gather_rows(x, graph.rowptr, graph.col, x.size(0), mean=True, order=graph.order, hub=graph.hub,
                                name="gather_fwd")
 
     @staticmethod
@@ -246,7 +274,7 @@ class _MeanAggFn(torch.autograd.Function):
         graph = ctx.graph
         g = g.contiguous().clone()
         ops.scale_rows_by_inv_deg_(g, graph.rowptr)
-        return ops.gather_rows(g, graph.t_rowptr, graph.t_col, ctx.n, mean=False, order=graph.t_order,
+        return ops.gather_rows(g, graph.t_rowptr, graph.t_col, ctx.n, mean=False, order=graph.t_order, hub=graph.t_hub,
                                name="gather_bwd"), None
 
 
@@ -293,7 +321,7 @@ class SageBlock(nn.Module):
                 raise TypeError("SageBlock post[0] must be an affine LayerNorm")
             p = _drop_p(drop)
             layers.append(((conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, ln.weight,
-                            ln.bias), (_act_slope(act), p, _new_seed() if p > 0 else 0,
+                            ln.bias), (_act_slope(act), p, _new_seed(x.device) if p > 0 else 0,
                                        float(ln.eps))))
         if grad and FUSE_BOUNDARIES and ops.branch_source(x) is None:
             # training: one autograd node for the stack (fused layer boundaries)

@@ -68,3 +68,56 @@ def run_oracle(ref, x, edge_index, gout):
     out.backward(gout.float())
     grads = {k: p.grad.clone() for k, p in ref.named_parameters()}
     return out.detach(), xr.grad.detach(), grads
+
+
+def bf16_oracle(ref, x, edge_index, gout, negative_slope, round_sum_first=False,
+                act_masks=None, stats=None, check_rows=None, store="bf16"):
+    """oracle/sage_bf16_ref.py on ``ref``'s parameters: (out, dx, grads).
+    ``store="fp32"``: the same restatement without storage rounding."""
+    from oracle.sage_bf16_ref import bf16_round, block_params, sageblock_fwd_bwd
+    return sageblock_fwd_bwd(block_params(ref), x.detach().cpu().float(), edge_index.cpu(),
+                             gout.detach().cpu().float(), negative_slope,
+                             store=bf16_round if store == "bf16" else None,
+                             round_sum_first=round_sum_first, act_masks=act_masks,
+                             stats=stats, check_rows=check_rows)
+
+
+def assert_bf16_close(name, got, want, atol=1e-2, rtol=1e-2):
+    """north_star's bf16 bar, element-wise: |got - want| <= atol + rtol |want|
+    against the bf16-storage oracle (like-for-like rounding points)."""
+    got = got.detach().float().cpu()
+    want = want.detach().float().cpu()
+    bad = (got - want).abs() > atol + rtol * want.abs()
+    if bool(bad.any()):
+        idx = bad.nonzero()[:5].tolist()
+        raise AssertionError(
+            f"{name}: {int(bad.sum())} of {bad.numel()} elements off by more than "
+            f"{atol} + {rtol}|ref| (max abs diff {(got - want).abs().max().item():.4g}); "
+            f"first at {idx}: got {[got[tuple(i)].item() for i in idx]}, "
+            f"want {[want[tuple(i)].item() for i in idx]}")
+
+
+def device_act_masks(blk, x, edge_index, rows=None):
+    """The device run's activation branch per layer, (layer output > 0), from
+    forwards of the block truncated after each layer (the same kernels, so
+    the same bits as inside the full block; the last one is checked against
+    the full forward by the caller).  For LeakyReLU / ReLU, output > 0 iff
+    the pre-activation > 0.  ``rows``: keep only these rows (device index)."""
+    import torch.nn as nn
+    from sldm_sage import SageBlock
+    hd = [blk.convs[0].in_channels] + [c.out_channels for c in blk.convs]
+    ns = blk.posts[0][1].negative_slope if isinstance(blk.posts[0][1], nn.LeakyReLU) else None
+    masks, outs = [], []
+    sd = blk.state_dict()
+    with torch.no_grad():
+        for depth in range(1, len(hd)):
+            part = SageBlock(hd[: depth + 1], None, ns)
+            part.load_state_dict({k: v for k, v in sd.items()
+                                  if int(k.split(".")[1]) < depth})
+            part = part.to(x.device).eval()
+            o = part(x.detach(), edge_index)
+            if rows is not None:
+                o = o[rows]
+            masks.append((o > 0).cpu())
+            outs.append(o)
+    return masks, outs

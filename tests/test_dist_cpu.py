@@ -24,13 +24,39 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, hdims, n, e, q, strategy="halo", chunks=4):
+def _graph(kind, n, e, f):
+    """Test graphs: "random" (uniform src/dst); "closed1" (W = 3, rows split
+    in thirds: rank 1's block [n/3, 2n/3) is a closed component -- its rows
+    exchange nothing -- while blocks 0 and 2 reference each other);
+    "powerlaw" (in-degrees Zipf-skewed: hubs at low ids)."""
+    from oracle.sage_ref import random_graph
+    ei, x = random_graph(n, e, f, seed=3)
+    if kind == "closed1":
+        g = torch.Generator().manual_seed(5)
+        a, b = n // 3, 2 * n // 3
+        src, dst = ei[0].clone(), ei[1].clone()
+        mid_d = (dst >= a) & (dst < b)
+        src[mid_d] = torch.randint(a, b, (int(mid_d.sum()),), generator=g)
+        mid_s = (src >= a) & (src < b) & ~mid_d
+        # edges leaving the middle block from outside it are redirected to block 0/2
+        outer = torch.cat([torch.arange(0, a), torch.arange(b, n)])
+        src[mid_s] = outer[torch.randint(0, outer.numel(), (int(mid_s.sum()),), generator=g)]
+        ei = torch.stack([src, dst])
+    elif kind == "powerlaw":
+        g = torch.Generator().manual_seed(6)
+        u = torch.rand(e, generator=g, dtype=torch.float64)
+        dst = ((1.0 + u * (n ** 0.5 - 1.0)) ** 2.0).floor().long().clamp(1, n) - 1
+        ei = torch.stack([ei[0], dst])
+    return ei, x
+
+
+def _worker(rank, world, port, hdims, n, e, q, strategy="halo", chunks=4, graph="random",
+            balance="cost"):
     sys.path[:0] = [HERE, os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "sldm-gnn_amd")]
     import torch.distributed as dist
 
     from _cpu_backend import CpuBackend
     from _helpers import oracle_block, run_oracle
-    from oracle.sage_ref import random_graph
     from sldm_sage import SageBlock
     from sldm_sage.dist import DistSageBlock, plan_partition
 
@@ -38,7 +64,7 @@ def _worker(rank, world, port, hdims, n, e, q, strategy="halo", chunks=4):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.manual_seed(0)
-        ei, x = random_graph(n, e, hdims[0], seed=3)
+        ei, x = _graph(graph, n, e, hdims[0])
         gout = torch.randn(n, hdims[-1], generator=torch.Generator().manual_seed(4))
         ref = oracle_block(hdims, 0.1)
         out_r, dx_r, grads_r = run_oracle(ref, x, ei, gout)
@@ -47,7 +73,12 @@ def _worker(rank, world, port, hdims, n, e, q, strategy="halo", chunks=4):
         if rank == 0:
             blk.load_state_dict(ref.state_dict())   # other ranks get it by broadcast
         part, info = plan_partition(ei, n, world, rank, hdims[0], 4, strategy=strategy,
-                                    backend=CpuBackend, chunks=chunks)
+                                    backend=CpuBackend, chunks=chunks, balance=balance)
+        if graph == "closed1" and rank == 1:
+            # nothing crosses this rank's boundary, yet it must join the
+            # exchanges the other ranks issue (decided globally)
+            assert part.halo_rows() == (0, 0) and sum(part.fwd_plan.send_counts) == 0
+            assert part.fwd_plan.active and part.bwd_plan.active
         assert info["strategy"] in ("halo", "feature", "replicate")
         if info["strategy"] == "replicate":      # the HIP SageBlock itself: GPU tests
             q.put((rank, "ok"))
@@ -73,12 +104,13 @@ def _worker(rank, world, port, hdims, n, e, q, strategy="halo", chunks=4):
         dist.destroy_process_group()
 
 
-def _run(world, n, hdims, strategy, chunks=4):
+def _run(world, n, hdims, strategy, chunks=4, graph="random", balance="cost"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker,
-                         args=(r, world, port, hdims, n, 6 * n, q, strategy, chunks))
+                         args=(r, world, port, hdims, n, 6 * n, q, strategy, chunks, graph,
+                               balance))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -92,6 +124,32 @@ def _run(world, n, hdims, strategy, chunks=4):
 @pytest.mark.parametrize("world,n", [(2, 300), (3, 301), (4, 97), (8, 203)])
 def test_dist_sageblock_matches_single_device(world, n):
     _run(world, n, [8, 12, 8], "halo")
+
+
+def test_halo_closed_component_rank_joins_exchange():
+    """a rank whose block exchanges nothing must still take part in
+    the halo all-to-alls the other ranks issue (global skip decision)."""
+    _run(3, 300, [8, 12, 8], "halo", graph="closed1", balance="rows")
+
+
+@pytest.mark.parametrize("world", [3, 4])
+def test_halo_cost_balanced_powerlaw(world):
+    """Cost-balanced row blocks (cumulative degree) on a skewed graph."""
+    _run(world, 400, [8, 8], "halo", graph="powerlaw", balance="cost")
+
+
+def test_row_bounds_balance_degree():
+    from sldm_sage.dist import row_bounds
+    n, e = 10_000, 200_000
+    ei, _ = _graph("powerlaw", n, e, 4)
+    b = row_bounds(ei, n, 4, "cost")
+    assert b[0] == 0 and b[-1] == n and all(b[i] <= b[i + 1] for i in range(4))
+    deg = torch.bincount(ei[1], minlength=n) + torch.bincount(ei[0], minlength=n) + 17
+    cost = [int(deg[b[r]:b[r + 1]].sum()) for r in range(4)]
+    assert max(cost) < 1.1 * sum(cost) / 4, cost
+    rows = row_bounds(ei, n, 4, "rows")
+    cost_rows = [int(deg[rows[r]:rows[r + 1]].sum()) for r in range(4)]
+    assert max(cost_rows) > 1.3 * max(cost)           # the hubs sit in block 0
 
 
 @pytest.mark.parametrize("world,n,chunks", [(2, 300, 4), (3, 301, 3), (4, 97, 1), (4, 10, 8),

@@ -177,3 +177,50 @@ def test_golden_fixture_matches_oracle(fn):
         g = torch.from_numpy(z["grad." + k])
         s = max(1.0, g.abs().max().item())
         torch.testing.assert_close(p.grad / s, g / s, atol=5e-5, rtol=5e-5)
+
+
+# ------------------------------------------------- bf16-storage oracle --
+@pytest.mark.parametrize("case", list(EDGE_CASES))
+@pytest.mark.parametrize("hdims,ns", [([6, 5, 4], 0.1), ([6, 8], None), ([6, 6, 6, 6], 0.2)])
+def test_bf16_oracle_unrounded_equals_fp32_oracle(case, hdims, ns):
+    """oracle/sage_bf16_ref.py with storage rounding off is the plain
+    reference: its hand-written backward must equal sage_ref's autograd."""
+    from oracle.sage_bf16_ref import block_params, sageblock_fwd_bwd
+    n = 40
+    ei = EDGE_CASES[case](n)
+    gen = torch.Generator().manual_seed(4)
+    x = torch.randn(n, hdims[0], generator=gen)
+    gout = torch.randn(n, hdims[-1], generator=gen)
+    ref = RefSageBlock(hdims, None, ns)
+    set_synthetic_params(ref, seed=2)
+    with torch.no_grad():
+        for post in ref.posts:
+            post[0].weight.uniform_(0.5, 1.5, generator=gen)
+            post[0].bias.uniform_(-0.5, 0.5, generator=gen)
+    xr = x.clone().requires_grad_(True)
+    out_r = ref(xr, ei)
+    out_r.backward(gout)
+    out, dx, grads = sageblock_fwd_bwd(block_params(ref), x, ei, gout, ns, store=None)
+    tol = dict(atol=2e-5, rtol=2e-5)
+    torch.testing.assert_close(out, out_r.detach(), **tol)
+    torch.testing.assert_close(dx, xr.grad, **tol)
+    for k, p in ref.named_parameters():
+        torch.testing.assert_close(grads[k], p.grad, **tol, msg=lambda m: f"{k}: {m}")
+
+
+def test_bf16_oracle_rounds_where_stored():
+    """With rounding on: outputs and the input grad are bf16 values, and the
+    result stays within bf16 resolution of the fp32 reference."""
+    from oracle.sage_bf16_ref import block_params, branch_margin, sageblock_fwd_bwd
+    hdims = [16, 16, 16]
+    ei, x = random_graph(300, 1500, 16, seed=7)
+    x = x.bfloat16().float()
+    gout = torch.randn(300, 16, generator=torch.Generator().manual_seed(8)).bfloat16().float()
+    ref = RefSageBlock(hdims, None, 0.1)
+    set_synthetic_params(ref, seed=2)
+    out, dx, grads = sageblock_fwd_bwd(block_params(ref), x, ei, gout, 0.1)
+    assert torch.equal(out, out.bfloat16().float()) and torch.equal(dx, dx.bfloat16().float())
+    out32, dx32, _ = sageblock_fwd_bwd(block_params(ref), x, ei, gout, 0.1, store=None)
+    s = out32.abs().max()
+    assert (out - out32).abs().max() < 2e-2 * s
+    assert 0 < branch_margin(block_params(ref), x, ei, 0.1) < 1e-2
