@@ -42,9 +42,9 @@ computations may take different sides, and LayerNorm's backward then spreads
 the difference over the row and the graph.  At full graph sizes such
 elements occur (C2: ~12.8 M pre-activations per layer).  ``act_masks`` (per
 layer, bool [N, F]: the device run's branch, e.g. its layer output > 0)
-resolves exactly those ties: where |y| < ambiguity (forward) or the
-backward's y from the stored xhat is within it, the oracle takes the given
-branch; everywhere else it keeps its own, and ``stats`` counts the elements
+resolves exactly those ties: where |y| < ambiguity the oracle takes the
+given branch in the forward (and, for fp32 storage, in the backward, which
+re-derives the same y); everywhere else it keeps its own, and ``stats`` counts the elements
 where the given branch disagrees with the oracle's outside the ambiguous
 band ("branch_disagreements", which a correct kernel keeps at 0) and the
 ambiguous elements resolved ("ambiguous").
@@ -82,16 +82,24 @@ def sageblock_fwd_bwd(layers: list[dict], x: torch.Tensor, edge_index: torch.Ten
                       gout: torch.Tensor, negative_slope: float | None = 0.1,
                       eps: float = 1e-5, store=bf16_round, round_sum_first: bool = False,
                       act_masks: list | None = None, ambiguity: float = 1e-5,
-                      stats: dict | None = None, check_rows: list | None = None):
+                      stats: dict | None = None, check_rows: list | None = None,
+                      layer_inputs: list | None = None):
     """Forward + backward of the block with storage rounding ``store``.
 
     Returns (out, dx, grads) with ``grads`` keyed like the state_dict
     (``convs.{i}.lin_l.weight`` ...), all fp32 on the CPU.  ``act_masks`` /
     ``ambiguity`` / ``stats``: branch ties (module docstring); ``check_rows``
     (per layer, bool [N] or None) limits the disagreement count to the rows
-    whose layer output is meaningful (a k-hop subgraph's exact rows)."""
+    whose layer output is meaningful (a k-hop subgraph's exact rows).
+    ``layer_inputs`` (per layer, [N, F] or None): teacher forcing -- layer
+    l > 0 reads the given tensor (the device run's layer l-1 output) instead
+    of the oracle's own, so each layer is compared like-for-like (a one-ulp
+    bf16 rounding difference of an input element would otherwise move later
+    pre-activations by ~1e-3 and flip genuine kink ties); ``stats`` then
+    records the largest relative difference between the oracle's own layer
+    output and the given one ("forward_rel_diff", on ``check_rows``)."""
     if stats is not None:
-        stats.update(ambiguous=0, branch_disagreements=0)
+        stats.update(ambiguous=0, branch_disagreements=0, forward_rel_diff=0.0)
     st = store or _identity
     f64 = torch.float64
     slope = 0.0 if negative_slope is None else float(negative_slope)
@@ -101,6 +109,16 @@ def sageblock_fwd_bwd(layers: list[dict], x: torch.Tensor, edge_index: torch.Ten
     h = st(x.detach().cpu().to(torch.float32)).to(f64)
     saved = []
     for p in layers:
+        li = len(saved)
+        if li > 0 and layer_inputs is not None and layer_inputs[li] is not None:
+            given_in = layer_inputs[li].detach().cpu().to(f64)
+            if stats is not None:
+                rel = (h - given_in).abs() / (1.0 + given_in.abs())
+                if check_rows is not None and check_rows[li - 1] is not None:
+                    rel = rel[check_rows[li - 1].cpu().bool()]
+                if rel.numel():
+                    stats["forward_rel_diff"] = max(stats["forward_rel_diff"], float(rel.max()))
+            h = given_in
         wl, wr = st(p["wl"].float()).to(f64), st(p["wr"].float()).to(f64)
         s = torch.zeros(n, h.size(1), dtype=torch.float32)
         s.index_add_(0, dst, h[src].float())                 # fp32 sum (CSR order)
@@ -138,8 +156,12 @@ def sageblock_fwd_bwd(layers: list[dict], x: torch.Tensor, edge_index: torch.Ten
         beta = layers[i]["beta"].to(f64)
         yb = xh * gamma + beta
         pos_b = yb > 0
-        if given is not None:
-            pos_b = torch.where(amb | (yb.abs() < ambiguity), given, pos_b)
+        if given is not None and store is None:
+            # fp32 storage: the device recomputes the forward's y exactly, so
+            # its backward branch is its forward branch.  (bf16: the branch
+            # comes from y = fma(bf16 xhat, gamma, beta), whose sign this
+            # fp64 evaluation reproduces exactly for the same stored xhat.)
+            pos_b = torch.where(amb, given, pos_b)
         dy = torch.where(pos_b, d, d * slope)
         gx = dy * gamma
         m1 = gx.mean(1, keepdim=True)

@@ -40,7 +40,14 @@ constexpr int kThreads = 512;
 constexpr int RW = 32;            // rows per wave
 constexpr int NTT = 16;           // 16-column MFMA tiles per wave (256 columns)
 constexpr int NSTW = 4;           // weight ring stages
-constexpr int DA = 4;             // activation register ring depth (k-steps)
+// Activation register ring depth (k-steps of A in flight per wave).  Any
+// DA >= NSTW keeps the steady-state count VM_BASE: A(s) is issued DA steps
+// ahead, before W(s) (NSTW-1 steps ahead), so the ops younger than W(s) are
+// the same 2 W + 3 A groups (header comment).
+#ifndef SLDM_STREAM_DA
+#define SLDM_STREAM_DA 4
+#endif
+constexpr int DA = SLDM_STREAM_DA;
 constexpr int SROW = 512 + 16;    // LN staging row stride in bytes (conflict-free b64 writes)
 
 enum { ST_LN = 0, ST_ROWSCALE = 1 };
@@ -111,7 +118,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
   // xhat, see loose_ok), ROWSCALE 2 x NTT/2 paired 16-B stores
   constexpr int S_EPI = MODE == ST_LN ? 32 : NTT;
   constexpr int VM_FIRST = VM_BASE + S_EPI > 63 ? 63 : VM_BASE + S_EPI;
-  static_assert(KSTEPS % NSTW == 0 && KSTEPS % DA == 0 && KSTEPS >= NSTW, "ring shape");
+  static_assert(KSTEPS % NSTW == 0 && KSTEPS % DA == 0 && KSTEPS >= NSTW && DA >= NSTW,
+                "ring shape");
   static_assert(MODE == ST_ROWSCALE || WN == 1, "LN needs the whole row in one wave");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -191,14 +199,17 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
     TileA p0;
     rows_of(tile, p0);
     // Same issue order as the steady state (A(s+1) right after W(s)), so the
-    // first tile's steps use the same counts: A(0), then W(s), A(s+1).
-    static_assert(DA == NSTW, "prologue interleave assumes DA == NSTW");
+    // first tile's steps use the same counts: A(0), then W(s), A(s+1); the
+    // remaining ring slots (DA > NSTW) after them -- younger ops only make
+    // the first steps' counts stricter.
     load_a(p0, 0, ar[0]);
 #pragma unroll
     for (int s = 0; s < NSTW - 1; ++s) {
       issue_w(s, s);
       load_a(p0, s + 1, ar[s + 1]);
     }
+#pragma unroll
+    for (int s = NSTW; s < DA; ++s) load_a(p0, s, ar[s]);
   }
 
   // The loose first-steps count is valid only when the previous epilogue

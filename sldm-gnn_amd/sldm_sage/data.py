@@ -14,8 +14,8 @@ dataset.py:85):
   become a tensor, anything else a list;
 * ``batch`` [N] (graph id per node), ``ptr`` [B+1] and ``num_graphs`` as in
   PyG, so ``batch.y.view(batch.num_graphs, L)`` (utils.py:222) works;
-* each graph's CSR pair (by destination, and by source for the backward) is
-  built once on the host (stable counting order = the GPU builder's order,
+* for graphs on the host, each graph's CSR pair (by destination, and by
+  source for the backward) is built once on the host (stable counting order = the GPU builder's order,
   bit for bit) and cached on the graph object; the batch's CSR is the
   concatenation of its graphs' CSRs with offsets -- equal to building it from
   the batched edge_index -- and ``GraphBatch.to(device)`` registers it for
@@ -201,7 +201,14 @@ def collate(data_list) -> GraphBatch:
         torch.arange(len(items), device=dev), torch.tensor(counts, device=dev))
     store["ptr"] = torch.as_tensor(offs, device=dev)
     csr = None
-    if "edge_index" in items[0]:
+    # The batch CSR is assembled on the host from per-graph host CSRs when the
+    # graphs live on the host (the DataLoader-worker case).  Graphs already on
+    # the GPU (dataset.py:77 loads with map_location=DEVICE) keep theirs off:
+    # reading every graph's edge_index back would cost one device sync per
+    # graph, where the SageBlock builds the batch CSR on the GPU with one.
+    if "edge_index" in items[0] and all(
+            getattr(d.get("edge_index"), "device", torch.device("cpu")).type == "cpu"
+            for d in items):
         parts = [graph_csr(data_list[i], items[i]["edge_index"], counts[i])
                  for i in range(len(items))]
         e_offs = np.zeros(len(items) + 1, np.int64)

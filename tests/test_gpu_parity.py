@@ -371,6 +371,8 @@ def _oracle_with_ties(ref, blk, x, xg, ei, gout, ns, out, store, rows=None, sub_
     resolved by the device run (oracle/sage_bf16_ref.py, "Activation-branch
     ties"): pre-activations within 1e-5 of the kink take the device's side;
     everywhere else the device's branch must equal the oracle's (asserted).
+    bf16 also teacher-forces each layer's input with the device's previous
+    layer output (asserting the oracle's own output within 1e-2 of it).
     ``rows`` / ``sub_ei`` / ``gout_sub``: run the oracle on a k-hop subgraph
     (device rows ``rows``), counting disagreements only on ``check_rows``."""
     eig = ei.to(DEV) if sub_ei is None else ei
@@ -378,11 +380,15 @@ def _oracle_with_ties(ref, blk, x, xg, ei, gout, ns, out, store, rows=None, sub_
     full_out = out.detach() if rows is None else out.detach()[rows]
     assert torch.equal(outs[-1], full_out), "truncated forwards differ from the block"
     stats = {}
+    # bf16: teacher-forced layer inputs (each layer like-for-like; the
+    # oracle's own layer outputs must still be within the bf16 bar)
+    forced = [None] + [o.float() for o in outs[:-1]] if store == "bf16" else None
     res = bf16_oracle(ref, xg.detach()[rows] if rows is not None else x,
                       ei if sub_ei is None else sub_ei,
                       gout if gout_sub is None else gout_sub, ns, act_masks=masks, stats=stats,
-                      check_rows=check_rows, store=store)
+                      check_rows=check_rows, store=store, layer_inputs=forced)
     assert stats["branch_disagreements"] == 0, stats
+    assert stats["forward_rel_diff"] <= 1e-2, stats
     return res
 
 
