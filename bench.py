@@ -279,19 +279,25 @@ def bench_gru(args, dev):
     forward + backward of the last hidden state (MIOpen; SURVEY §8f row 4:
     measure before any hand kernel).  Roofline: the gate GEMMs' FLOP against
     the dense fp32 MFMA peak."""
+    from sldm_sage import GRU
     N, T, I, H = PACKS_PER_BATCH * VEHICLES[1], 100, 6, 96
     gen = torch.Generator(device=dev).manual_seed(0)
     torch.manual_seed(0)
-    gru = torch.nn.GRU(I, H, 1, batch_first=True).to(dev)
+    ref = torch.nn.GRU(I, H, 1, batch_first=True).to(dev)
+    ours = GRU(I, H, 1, batch_first=True).to(dev)
+    ours.load_state_dict(ref.state_dict())
     x = torch.randn(N, T, I, generator=gen, device=dev)
     g = torch.randn(N, H, generator=gen, device=dev)
 
-    def step():
-        gru.zero_grad(set_to_none=True)
-        _, hl = gru(x)
-        hl[-1].backward(g)
+    def stepper(gru):
+        def step():
+            gru.zero_grad(set_to_none=True)
+            _, hl = gru(x)
+            hl[-1].backward(g)
+        return step
 
-    t = _time_steps(step, args.warmup, args.steps)
+    t = _time_steps(stepper(ours), args.warmup, args.steps)
+    t_miopen = _time_steps(stepper(ref), min(args.warmup, 2), min(args.steps, 5))
     flop_fwd = 2.0 * N * T * 3 * (I * H + H * H)
     flop = 3 * flop_fwd                               # fwd + dX/dH + dW
     ach = flop / t / 1e12
@@ -300,7 +306,10 @@ def bench_gru(args, dev):
             "unit": "sequences/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic x~N(0,1)",
-            "config": {"workload": f"nn.GRU({I}->{H}) over [{N}, {T}, {I}], fwd+bwd (MIOpen)"},
+            "config": {"workload": f"GRU({I}->{H}) over [{N}, {T}, {I}], fwd + bwd of h_n "
+                                   "(grusage.py:160-161), sldm_sage.GRU (gru.hip)"},
+            "torch_miopen": {"ms_per_step": round(t_miopen * 1e3, 3),
+                             "value": round(N / t_miopen, 1)},
             "roofline": {"bound": "mfma", "achieved": round(ach, 3), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(ach / peak, 5), "traffic": None,
                          "note": "gate GEMM FLOP (3 x fwd) / dense fp32 MFMA peak; the T = 100 "

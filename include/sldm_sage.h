@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SLDM_ABI_VERSION 3
+#define SLDM_ABI_VERSION 4
 
 enum sldm_dtype { SLDM_F32 = 0, SLDM_BF16 = 1 };
 enum sldm_status { SLDM_OK = 0, SLDM_ERR_ARG = 1, SLDM_ERR_HIP = 2 };
@@ -269,6 +269,39 @@ int sldm_radius_edges(const float* pos, int64_t pos_sv, int64_t pos_st, int64_t 
                       int64_t* edge_index, int64_t capacity, float* edge_attr,
                       int32_t* num_edges, void* workspace, size_t workspace_bytes,
                       void* stream);
+
+/* ------------------------------------------------------------------- GRU ---
+ * The model's trajectory GRU: torch.nn.GRU(I -> H,
+ * num_layers=1) as built at grusage.py:66-71 and called at :160-161
+ * (gru_out, hlast = self.gru(x)), fp32, PyTorch's cell (aten RNN.cpp):
+ *   r = s(x W_ir^T + b_ir + h W_hr^T + b_hr), z = s(... _iz ... _hz),
+ *   n = tanh(x W_in^T + b_in + r (h W_hn^T + b_hn)), h' = (h - n) z + n.
+ * x[n, t, i] at x + n*ldx_n + t*ldx_t + i (batch_first or time-major);
+ * W_ih [3H, I], W_hh [3H, H] row-major in PyTorch's gate order (r, z, n);
+ * biases and h0 [N, H] nullable (zeros).  out[n, t, :] = h_t (ldo_n, ldo_t),
+ * h_n [N, H] nullable.  gates (nullable; needed by the backward):
+ * sldm_gru_workspace_bytes(N, T, H) bytes.  Requires 1 <= I <= 16 and H a
+ * multiple of 16 in [16, 96]. */
+size_t sldm_gru_workspace_bytes(int64_t N, int64_t T, int64_t H);
+int sldm_gru_fwd(const float* x, int64_t ldx_n, int64_t ldx_t, int64_t N, int64_t T, int64_t I,
+                 int64_t H, const float* w_ih, const float* w_hh, const float* b_ih,
+                 const float* b_hh, const float* h0, float* out, int64_t ldo_n, int64_t ldo_t,
+                 float* h_n, float* gates, void* stream);
+
+/* Backward of sldm_gru_fwd (autograd of nn.GRU): dout [N, T, H] (ldd_n, ldd_t)
+ * and dh_n [N, H] are the upstream gradients (either nullable = zero); writes
+ * dW_ih, dW_hh (overwritten, fp32), db_ih, db_hh (nullable), dh0 and dx
+ * (nullable; dx at dx + n*lddx_n + t*lddx_t + i).  Weight gradients are summed
+ * over per-workgroup partials in a fixed order (deterministic).
+ * workspace: sldm_gru_bwd_workspace_bytes(N, T, I, H, dx != NULL). */
+size_t sldm_gru_bwd_workspace_bytes(int64_t N, int64_t T, int64_t I, int64_t H, int need_dx);
+int sldm_gru_bwd(const float* x, int64_t ldx_n, int64_t ldx_t, int64_t N, int64_t T, int64_t I,
+                 int64_t H, const float* w_ih, const float* w_hh, const float* h0,
+                 const float* out, int64_t ldo_n, int64_t ldo_t, const float* gates,
+                 const float* dout, int64_t ldd_n, int64_t ldd_t, const float* dh_n, float* dx,
+                 int64_t lddx_n, int64_t lddx_t, float* dh0, float* dw_ih, float* dw_hh,
+                 float* db_ih, float* db_hh, void* workspace, size_t workspace_bytes,
+                 void* stream);
 
 #ifdef __cplusplus
 }

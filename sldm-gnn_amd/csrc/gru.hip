@@ -1,0 +1,508 @@
+// GRU over the vehicle trajectories: the model's
+// torch.nn.GRU(dynamic_features_num -> gru_hidden_size, 1 layer, batch_first)
+// (grusage.py:66-71, called at :160-161), forward and backward.
+//
+// torch's GRU (MIOpen) runs the T = 100 recurrence at ~1 % of the fp32 MFMA
+// peak on the vehicle batch ([9600, 100, 6] -> 96, bench.py --config gru:
+// 101 ms per fwd + bwd).  Here one workgroup owns a 16-row tile of sequences
+// for the whole recurrence, one wave per 16 hidden units:
+//
+//  * the recurrent weights never leave registers: wave w holds the MFMA
+//    B-fragments of W_hh rows {g*H + 16w + c} (gates r, z, n) for all k --
+//    3 H/4 VGPRs -- and of W_ih likewise (3 KI);
+//  * h_t lives in a double-buffered LDS image laid out as MFMA A-fragments
+//    (one ds_read_b128 brings 4 k-steps), written by the wave that owns each
+//    hidden tile, one barrier per step;
+//  * per step and wave: KI + 3 H/4 ... x3 v_mfma_f32_16x16x4_f32 (exact fp32,
+//    k-ordered fma chains; no reduced-precision path on gfx950), then the
+//    gate math of its 16 x 16 outputs in registers: the r / z / n columns of
+//    one hidden unit sit in the same lane of three accumulators.
+//  PyTorch's cell (aten RNN.cpp gru_cell): r = s(gi_r + gh_r),
+//  z = s(gi_z + gh_z), n = tanh(gi_n + r * gh_n), h' = (h - n) * z + n, with
+//  gi = x W_ih^T + b_ih and gh = h W_hh^T + b_hh.
+//
+// The forward stores every h_t (the output) and, for the backward, the gate
+// values r, z, n and gh_n in a lane-native workspace.  The backward runs the
+// recurrence in reverse with the weight-gradient tiles dW_hh (3 H/4 regs),
+// dW_ih, db as MFMA accumulators across all steps (the C-layout dGh is the A
+// operand of dGh^T h_{t-1} with the 4 register rows as the k index) and
+// W_hh's fragments for dh_{t-1} = dGh W_hh in LDS (beside the accumulators
+// they would take the wave to 295 VGPRs); per-workgroup partials are summed
+// by a reduce kernel in a fixed order (deterministic).
+//
+// Sizes: H = 16 NW (NW = 1..6 waves), I <= 16 (KI = ceil(I / 4) k-steps).
+#include "common.hpp"
+
+namespace {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float sigm(float v) { return 1.0f / (1.0f + expf(-v)); }
+
+// LDS image of a [16 rows][K] operand as MFMA A-fragments: k-step q of lane l
+// is element (row l & 15, k = 4q + (l >> 4)); four consecutive k-steps of a
+// lane are one 16-B word: float index ((q >> 2) * 64 + l) * 4 + (q & 3).
+__device__ __forceinline__ int aimg(int row, int k) {
+  const int q = k >> 2, lane = row + 16 * (k & 3);
+  return ((q >> 2) * 64 + lane) * 4 + (q & 3);
+}
+
+template <int NW, int KI>
+__global__ __launch_bounds__(64 * NW) void gru_fwd_kernel(
+    const float* __restrict__ x, int64_t ldxn, int64_t ldxt, int64_t N, int T, int I,
+    const float* __restrict__ w_ih, const float* __restrict__ w_hh,
+    const float* __restrict__ b_ih, const float* __restrict__ b_hh,
+    const float* __restrict__ h0, float* __restrict__ out, int64_t ldon, int64_t ldot,
+    float* __restrict__ h_n, float* __restrict__ gates) {
+  constexpr int H = 16 * NW;
+  constexpr int KH = H / 4;                 // k-steps over the hidden dim
+  __shared__ __attribute__((aligned(16))) float himg[2][KH * 64];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int c = lane & 15, g4 = lane >> 4;
+  const int j = 16 * w + c;                 // this lane's hidden unit
+  const int64_t r0 = (int64_t)blockIdx.x * 16;
+
+  // weights (B-fragments: B[k = 4q + g4][col c] = W[g H + j][k])
+  float whh[3][KH], wih[3][KI];
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+#pragma unroll
+    for (int q = 0; q < KH; ++q) whh[g][q] = w_hh[(int64_t)(g * H + j) * H + 4 * q + g4];
+#pragma unroll
+    for (int q = 0; q < KI; ++q) {
+      const int k = 4 * q + g4;
+      wih[g][q] = k < I ? w_ih[(int64_t)(g * H + j) * I + k] : 0.f;
+    }
+  }
+  float bias[4];                            // r, z (ih + hh), n_ih, n_hh
+  bias[0] = (b_ih ? b_ih[j] : 0.f) + (b_hh ? b_hh[j] : 0.f);
+  bias[1] = (b_ih ? b_ih[H + j] : 0.f) + (b_hh ? b_hh[H + j] : 0.f);
+  bias[2] = b_ih ? b_ih[2 * H + j] : 0.f;
+  bias[3] = b_hh ? b_hh[2 * H + j] : 0.f;
+
+  // own h (C-layout: rows 4 g4 + r, column j) and the initial LDS image
+  float hp[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t row = r0 + 4 * g4 + r;
+    hp[r] = (h0 && row < N) ? h0[row * H + j] : 0.f;
+    himg[0][aimg(4 * g4 + r, j)] = hp[r];
+  }
+  // x operand (A: row c, k = 4q + g4), one step ahead
+  const int64_t xrow = min(r0 + c, N - 1);
+  auto load_x = [&](int t, float (&xa)[KI]) {
+#pragma unroll
+    for (int q = 0; q < KI; ++q) {
+      const int k = 4 * q + g4;
+      xa[q] = (k < I && t < T) ? x[xrow * ldxn + (int64_t)t * ldxt + k] : 0.f;
+    }
+  };
+  float xa[KI], xn[KI];
+  load_x(0, xa);
+  __syncthreads();
+
+  for (int t = 0; t < T; ++t) {
+    load_x(t + 1, xn);
+    const float* hi = himg[t & 1];
+    f4v ar = {0.f, 0.f, 0.f, 0.f}, az = ar, an = ar, ahn = ar;
+#pragma unroll
+    for (int q = 0; q < KI; ++q) {
+      ar = mfma4(xa[q], wih[0][q], ar);
+      az = mfma4(xa[q], wih[1][q], az);
+      an = mfma4(xa[q], wih[2][q], an);
+    }
+#pragma unroll
+    for (int qq = 0; qq < KH / 4; ++qq) {
+      const f4v a4 = *reinterpret_cast<const f4v*>(hi + (qq * 64 + lane) * 4);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = 4 * qq + u;
+        ar = mfma4(a4[u], whh[0][q], ar);
+        az = mfma4(a4[u], whh[1][q], az);
+        ahn = mfma4(a4[u], whh[2][q], ahn);
+      }
+    }
+    float* ho = himg[(t + 1) & 1];
+    f4v gr, gz, gn, gh;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float rr = sigm(ar[r] + bias[0]);
+      const float zz = sigm(az[r] + bias[1]);
+      const float hn = ahn[r] + bias[3];
+      const float nn = tanhf(an[r] + bias[2] + rr * hn);
+      const float hv = (hp[r] - nn) * zz + nn;
+      gr[r] = rr; gz[r] = zz; gn[r] = nn; gh[r] = hn;
+      hp[r] = hv;
+      ho[aimg(4 * g4 + r, j)] = hv;
+      const int64_t row = r0 + 4 * g4 + r;
+      if (row < N) out[row * ldon + (int64_t)t * ldot + j] = hv;
+    }
+    if (gates) {
+      f4v* gp = reinterpret_cast<f4v*>(gates) +
+                ((((int64_t)t * gridDim.x + blockIdx.x) * NW + w) * 4) * 64 + lane;
+      gp[0] = gr; gp[64] = gz; gp[128] = gn; gp[192] = gh;
+    }
+#pragma unroll
+    for (int q = 0; q < KI; ++q) xa[q] = xn[q];
+    __syncthreads();
+  }
+  if (h_n) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = r0 + 4 * g4 + r;
+      if (row < N) h_n[row * H + j] = hp[r];
+    }
+  }
+}
+
+// Backward.  Per step (t descending), wave w, lane (c, g4), rows 4 g4 + r:
+//   dh   = carry + dout[t]           (carry = dh_n at t = T-1)
+//   dn   = dh (1 - z),  dz = dh (h_{t-1} - n),  dh_{t-1} <- dh z
+//   dan  = dn (1 - n^2), dr = dan gh_n, dar = dr r (1 - r), daz = dz z (1 - z)
+//   dGi  = [dar, daz, dan],  dGh = [dar, daz, dan r]
+//   dh_{t-1} += dGh W_hh                      (LDS image of dGh, W_hh frags)
+//   dW_hh += dGh^T h_{t-1}, dW_ih += dGi^T x_t, db += column sums
+template <int NW, int KI>
+__global__ __launch_bounds__(64 * NW) void gru_bwd_kernel(
+    const float* __restrict__ x, int64_t ldxn, int64_t ldxt, int64_t N, int T, int I,
+    const float* __restrict__ w_hh, const float* __restrict__ h0,
+    const float* __restrict__ out, int64_t ldon, int64_t ldot, const float* __restrict__ gates,
+    const float* __restrict__ dout, int64_t lddn, int64_t lddt, const float* __restrict__ dh_n,
+    float* __restrict__ dh0, float* __restrict__ dgi, float* __restrict__ part) {
+  constexpr int H = 16 * NW;
+  constexpr int KG = 3 * H / 4;             // k-steps over the 3H gate columns
+  // LDS (dynamic, gru_bwd_lds_bytes): dGh A-fragment image [2][KG*64],
+  // h_{t-1} C-layout tiles [2][NW*256], and this workgroup's copy of the
+  // dGh W_hh B-fragments [NW][KG/4][64][4] -- 3 H^2 floats (110.6 KB at
+  // H = 96) that do not fit in registers beside the dW_hh accumulators.
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float (*gimg)[KG * 64] = reinterpret_cast<float (*)[KG * 64]>(lds);
+  float (*pimg)[NW * 256] = reinterpret_cast<float (*)[NW * 256]>(lds + 2 * KG * 64);
+  float* wimg = lds + 2 * KG * 64 + 2 * NW * 256;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int c = lane & 15, g4 = lane >> 4;
+  const int j = 16 * w + c;
+  const int64_t r0 = (int64_t)blockIdx.x * 16;
+
+  // B-fragments of dGh W_hh: B[k = gate column 4q + g4][col j] = W_hh[4q + g4][j]
+  float* wmine = wimg + (int64_t)w * KG * 64;
+#pragma unroll 4
+  for (int q = 0; q < KG; ++q)
+    wmine[((q >> 2) * 64 + lane) * 4 + (q & 3)] = w_hh[(int64_t)(4 * q + g4) * H + j];
+
+  f4v dwh[3][NW], dwi[3];
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+    dwi[g] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < NW; ++kt) dwh[g][kt] = f4v{0.f, 0.f, 0.f, 0.f};
+  }
+  float db[4] = {0.f, 0.f, 0.f, 0.f};       // r, z, n_ih, n_hh column sums
+
+  bool live[4];
+  float dh[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t row = r0 + 4 * g4 + r;
+    live[r] = row < N;
+    dh[r] = (dh_n && live[r]) ? dh_n[row * H + j] : 0.f;
+  }
+  // x as the B operand of dW_ih: B[k <-> row 4 g4 + r][col i = c]
+  auto load_x = [&](int t, float (&xb)[4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = min(r0 + 4 * g4 + r, N - 1);
+      xb[r] = (c < I) ? x[row * ldxn + (int64_t)t * ldxt + c] : 0.f;
+    }
+  };
+
+  for (int t = T - 1; t >= 0; --t) {
+    const int b = t & 1;
+    const f4v* gp = reinterpret_cast<const f4v*>(gates) +
+                    ((((int64_t)t * gridDim.x + blockIdx.x) * NW + w) * 4) * 64 + lane;
+    const f4v gr = gp[0], gz = gp[64], gn = gp[128], gh = gp[192];
+    float hp[4], xb[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = min(r0 + 4 * g4 + r, N - 1);
+      hp[r] = t > 0 ? out[row * ldon + (int64_t)(t - 1) * ldot + j] : (h0 ? h0[row * H + j] : 0.f);
+      if (dout && live[r]) dh[r] += dout[row * lddn + (int64_t)t * lddt + j];
+    }
+    load_x(t, xb);
+    f4v dar, daz, dan, dghn;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float d = live[r] ? dh[r] : 0.f;
+      const float dn = d * (1.f - gz[r]);
+      const float dz = d * (hp[r] - gn[r]);
+      const float an = dn * (1.f - gn[r] * gn[r]);
+      const float drr = an * gh[r];
+      dar[r] = drr * gr[r] * (1.f - gr[r]);
+      daz[r] = dz * gz[r] * (1.f - gz[r]);
+      dan[r] = an;
+      dghn[r] = an * gr[r];
+      dh[r] = d * gz[r];                    // direct path; + dGh W_hh below
+      db[0] += dar[r];
+      db[1] += daz[r];
+      db[2] += dan[r];
+      db[3] += dghn[r];
+      // dGh image (A-fragments over the 3H gate columns) and h_{t-1} tile
+      gimg[b][aimg(4 * g4 + r, j)] = dar[r];
+      gimg[b][aimg(4 * g4 + r, H + j)] = daz[r];
+      gimg[b][aimg(4 * g4 + r, 2 * H + j)] = dghn[r];
+    }
+    *reinterpret_cast<f4v*>(&pimg[b][(w * 64 + lane) * 4]) = f4v{hp[0], hp[1], hp[2], hp[3]};
+    if (dgi) {                              // dx needs dGi: [N, T, 3H] in (row, t) order
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = r0 + 4 * g4 + r;
+        if (!live[r]) continue;
+        float* o = dgi + (row * T + t) * (int64_t)(3 * H);
+        o[j] = dar[r];
+        o[H + j] = daz[r];
+        o[2 * H + j] = dan[r];
+      }
+    }
+    __syncthreads();
+
+    // dh_{t-1} += dGh W_hh (rows 4 g4 + r, column j)
+    f4v acc = {0.f, 0.f, 0.f, 0.f};
+    const float* gi = gimg[b];
+#pragma unroll
+    for (int qq = 0; qq < KG / 4; ++qq) {
+      const f4v a4 = *reinterpret_cast<const f4v*>(gi + (qq * 64 + lane) * 4);
+      const f4v b4 = *reinterpret_cast<const f4v*>(wmine + (qq * 64 + lane) * 4);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = mfma4(a4[u], b4[u], acc);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dh[r] += acc[r];
+
+    // dW_hh[g H + 16 w + c'][16 kt + c''] += sum_rows dGh h_{t-1}: A = this
+    // lane's dGh registers (k-step r <-> row 4 g4 + r), B = h_{t-1} tile kt
+#pragma unroll
+    for (int kt = 0; kt < NW; ++kt) {
+      const f4v hb = *reinterpret_cast<const f4v*>(&pimg[b][(kt * 64 + lane) * 4]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dwh[0][kt] = mfma4(dar[r], hb[r], dwh[0][kt]);
+        dwh[1][kt] = mfma4(daz[r], hb[r], dwh[1][kt]);
+        dwh[2][kt] = mfma4(dghn[r], hb[r], dwh[2][kt]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      dwi[0] = mfma4(dar[r], xb[r], dwi[0]);
+      dwi[1] = mfma4(daz[r], xb[r], dwi[1]);
+      dwi[2] = mfma4(dan[r], xb[r], dwi[2]);
+    }
+  }
+  if (dh0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = r0 + 4 * g4 + r;
+      if (live[r]) dh0[row * H + j] = dh[r];
+    }
+  }
+  // per-workgroup partials: [3H][H] dW_hh | [3H][16] dW_ih | [4][H] db
+  // (accumulator D[row c'][col c''] = lane c'' of register 4 g4 + i)
+  float* p = part + (int64_t)blockIdx.x * (3 * H * H + 3 * H * 16 + 4 * H);
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int crow = g * H + 16 * w + 4 * g4 + i;
+#pragma unroll
+      for (int kt = 0; kt < NW; ++kt) p[crow * H + 16 * kt + c] = dwh[g][kt][i];
+      p[3 * H * H + crow * 16 + c] = dwi[g][i];
+    }
+  }
+  // column sums: reduce the four row groups (g4) of each column
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float v = db[k];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (g4 == 0) p[3 * H * H + 3 * H * 16 + k * H + j] = v;
+  }
+}
+
+// Sum the per-workgroup partials in workgroup order (deterministic) into
+// dW_hh [3H][H], dW_ih [3H][I], db_ih [3H], db_hh [3H].
+__global__ __launch_bounds__(256) void gru_reduce_kernel(const float* __restrict__ part,
+                                                         int64_t nparts, int H, int I,
+                                                         float* __restrict__ dw_ih,
+                                                         float* __restrict__ dw_hh,
+                                                         float* __restrict__ db_ih,
+                                                         float* __restrict__ db_hh) {
+  const int64_t stride = 3 * H * H + 3 * H * 16 + 4 * H;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= stride) return;
+  float s = 0.f;
+  for (int64_t p = 0; p < nparts; ++p) s += part[p * stride + e];
+  if (e < 3 * H * H) {
+    dw_hh[e] = s;
+    return;
+  }
+  int64_t f = e - 3 * H * H;
+  if (f < 3 * H * 16) {
+    const int64_t crow = f / 16, i = f % 16;
+    if (i < I) dw_ih[crow * I + i] = s;
+    return;
+  }
+  f -= 3 * H * 16;
+  const int k = (int)(f / H), jj = (int)(f % H);
+  // k: 0 = r (ih and hh), 1 = z (ih and hh), 2 = n_ih, 3 = n_hh
+  if (k < 2) {
+    if (db_ih) db_ih[k * H + jj] = s;
+    if (db_hh) db_hh[k * H + jj] = s;
+  } else if (k == 2) {
+    if (db_ih) db_ih[2 * H + jj] = s;
+  } else if (db_hh) {
+    db_hh[2 * H + jj] = s;
+  }
+}
+
+// dx[n, t, i] = sum_c dGi[n, t, c] W_ih[c, i]  (only when x needs a gradient)
+__global__ __launch_bounds__(256) void gru_dx_kernel(const float* __restrict__ dgi,
+                                                     const float* __restrict__ w_ih, int64_t rows,
+                                                     int H, int I, float* __restrict__ dx,
+                                                     int64_t T, int64_t lddxn, int64_t lddxt) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= rows * I) return;
+  const int64_t rt = e / I;
+  const int i = (int)(e % I);
+  const float* g = dgi + rt * 3 * H;
+  float s = 0.f;
+  for (int k = 0; k < 3 * H; ++k) s = fmaf(g[k], w_ih[(int64_t)k * I + i], s);
+  const int64_t n = rt / T, t = rt % T;
+  dx[n * lddxn + t * lddxt + i] = s;
+}
+
+template <int NW>
+int launch_fwd(int ki, dim3 grid, hipStream_t st, const float* x, int64_t ldxn, int64_t ldxt,
+               int64_t N, int T, int I, const float* w_ih, const float* w_hh, const float* b_ih,
+               const float* b_hh, const float* h0, float* out, int64_t ldon, int64_t ldot,
+               float* h_n, float* gates) {
+#define SLDM_GRU_F(KI)                                                                       \
+  gru_fwd_kernel<NW, KI><<<grid, 64 * NW, 0, st>>>(x, ldxn, ldxt, N, T, I, w_ih, w_hh, b_ih, \
+                                                   b_hh, h0, out, ldon, ldot, h_n, gates)
+  switch (ki) {
+    case 1: SLDM_GRU_F(1); break;
+    case 2: SLDM_GRU_F(2); break;
+    case 3: SLDM_GRU_F(3); break;
+    default: SLDM_GRU_F(4); break;
+  }
+#undef SLDM_GRU_F
+  SLDM_LAUNCH_CHECK("gru_fwd_kernel");
+  return SLDM_OK;
+}
+
+template <int NW>
+int launch_bwd(dim3 grid, hipStream_t st, const float* x, int64_t ldxn, int64_t ldxt, int64_t N,
+               int T, int I, const float* w_hh, const float* h0, const float* out, int64_t ldon,
+               int64_t ldot, const float* gates, const float* dout, int64_t lddn, int64_t lddt,
+               const float* dh_n, float* dh0, float* dgi, float* part) {
+  constexpr int H = 16 * NW;
+  constexpr size_t lds = sizeof(float) * (2 * (3 * H / 4) * 64 + 2 * NW * 256 + 3 * H * H);
+  static_assert(lds <= 160 * 1024, "GRU backward LDS budget");
+  auto kern = gru_bwd_kernel<NW, 1>;
+  SLDM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  kern<<<grid, 64 * NW, lds, st>>>(x, ldxn, ldxt, N, T, I, w_hh, h0, out, ldon, ldot, gates,
+                                   dout, lddn, lddt, dh_n, dh0, dgi, part);
+  SLDM_LAUNCH_CHECK("gru_bwd_kernel");
+  return SLDM_OK;
+}
+
+bool gru_shape_ok(int64_t N, int64_t T, int64_t I, int64_t H) {
+  return N > 0 && T > 0 && I >= 1 && I <= 16 && H >= 16 && H <= 96 && H % 16 == 0 &&
+         N < ((int64_t)1 << 31) && T < ((int64_t)1 << 24);
+}
+
+}  // namespace
+
+extern "C" size_t sldm_gru_workspace_bytes(int64_t N, int64_t T, int64_t H) {
+  if (N <= 0 || T <= 0 || H <= 0) return 16;
+  const int64_t tiles = (N + 15) / 16;
+  return (size_t)(T * tiles * (H / 16) * 4 * 64 * 4) * sizeof(float);
+}
+
+extern "C" int sldm_gru_fwd(const float* x, int64_t ldx_n, int64_t ldx_t, int64_t N, int64_t T,
+                            int64_t I, int64_t H, const float* w_ih, const float* w_hh,
+                            const float* b_ih, const float* b_hh, const float* h0, float* out,
+                            int64_t ldo_n, int64_t ldo_t, float* h_n, float* gates,
+                            void* stream_) {
+  SLDM_REQUIRE(gru_shape_ok(N, T, I, H),
+               "sldm_gru_fwd: unsupported shape N=%lld T=%lld I=%lld H=%lld (1 <= I <= 16, "
+               "H in 16..96 a multiple of 16)", (long long)N, (long long)T, (long long)I,
+               (long long)H);
+  SLDM_REQUIRE(x && w_ih && w_hh && out, "sldm_gru_fwd: NULL argument");
+  hipStream_t st = sldm::as_stream(stream_);
+  const dim3 grid((unsigned)((N + 15) / 16));
+  const int ki = (int)((I + 3) / 4);
+  const int t = (int)T, i = (int)I;
+  switch (H / 16) {
+    case 1: return launch_fwd<1>(ki, grid, st, x, ldx_n, ldx_t, N, t, i, w_ih, w_hh, b_ih, b_hh, h0, out, ldo_n, ldo_t, h_n, gates);
+    case 2: return launch_fwd<2>(ki, grid, st, x, ldx_n, ldx_t, N, t, i, w_ih, w_hh, b_ih, b_hh, h0, out, ldo_n, ldo_t, h_n, gates);
+    case 3: return launch_fwd<3>(ki, grid, st, x, ldx_n, ldx_t, N, t, i, w_ih, w_hh, b_ih, b_hh, h0, out, ldo_n, ldo_t, h_n, gates);
+    case 4: return launch_fwd<4>(ki, grid, st, x, ldx_n, ldx_t, N, t, i, w_ih, w_hh, b_ih, b_hh, h0, out, ldo_n, ldo_t, h_n, gates);
+    case 5: return launch_fwd<5>(ki, grid, st, x, ldx_n, ldx_t, N, t, i, w_ih, w_hh, b_ih, b_hh, h0, out, ldo_n, ldo_t, h_n, gates);
+    default: return launch_fwd<6>(ki, grid, st, x, ldx_n, ldx_t, N, t, i, w_ih, w_hh, b_ih, b_hh, h0, out, ldo_n, ldo_t, h_n, gates);
+  }
+}
+
+extern "C" size_t sldm_gru_bwd_workspace_bytes(int64_t N, int64_t T, int64_t I, int64_t H,
+                                               int need_dx) {
+  if (N <= 0 || T <= 0 || H <= 0) return 16;
+  const int64_t tiles = (N + 15) / 16;
+  size_t b = (size_t)tiles * (3 * H * H + 3 * H * 16 + 4 * H) * sizeof(float);
+  if (need_dx) b += (size_t)N * T * 3 * H * sizeof(float);
+  return b;
+}
+
+extern "C" int sldm_gru_bwd(const float* x, int64_t ldx_n, int64_t ldx_t, int64_t N, int64_t T,
+                            int64_t I, int64_t H, const float* w_ih, const float* w_hh,
+                            const float* h0, const float* out, int64_t ldo_n, int64_t ldo_t,
+                            const float* gates, const float* dout, int64_t ldd_n, int64_t ldd_t,
+                            const float* dh_n, float* dx, int64_t lddx_n, int64_t lddx_t,
+                            float* dh0, float* dw_ih, float* dw_hh, float* db_ih, float* db_hh,
+                            void* workspace, size_t workspace_bytes, void* stream_) {
+  SLDM_REQUIRE(gru_shape_ok(N, T, I, H), "sldm_gru_bwd: unsupported shape");
+  SLDM_REQUIRE(x && w_ih && w_hh && out && gates && dw_ih && dw_hh && workspace,
+               "sldm_gru_bwd: NULL argument");
+  SLDM_REQUIRE(workspace_bytes >= sldm_gru_bwd_workspace_bytes(N, T, I, H, dx != nullptr),
+               "sldm_gru_bwd: workspace too small");
+  hipStream_t st = sldm::as_stream(stream_);
+  const int64_t tiles = (N + 15) / 16;
+  const dim3 grid((unsigned)tiles);
+  float* part = reinterpret_cast<float*>(workspace);
+  float* dgi = dx ? part + tiles * (3 * H * H + 3 * H * 16 + 4 * H) : nullptr;
+  const int t = (int)T, i = (int)I;
+  int rc;
+  switch (H / 16) {
+    case 1: rc = launch_bwd<1>(grid, st, x, ldx_n, ldx_t, N, t, i, w_hh, h0, out, ldo_n, ldo_t, gates, dout, ldd_n, ldd_t, dh_n, dh0, dgi, part); break;
+    case 2: rc = launch_bwd<2>(grid, st, x, ldx_n, ldx_t, N, t, i, w_hh, h0, out, ldo_n, ldo_t, gates, dout, ldd_n, ldd_t, dh_n, dh0, dgi, part); break;
+    case 3: rc = launch_bwd<3>(grid, st, x, ldx_n, ldx_t, N, t, i, w_hh, h0, out, ldo_n, ldo_t, gates, dout, ldd_n, ldd_t, dh_n, dh0, dgi, part); break;
+    case 4: rc = launch_bwd<4>(grid, st, x, ldx_n, ldx_t, N, t, i, w_hh, h0, out, ldo_n, ldo_t, gates, dout, ldd_n, ldd_t, dh_n, dh0, dgi, part); break;
+    case 5: rc = launch_bwd<5>(grid, st, x, ldx_n, ldx_t, N, t, i, w_hh, h0, out, ldo_n, ldo_t, gates, dout, ldd_n, ldd_t, dh_n, dh0, dgi, part); break;
+    default: rc = launch_bwd<6>(grid, st, x, ldx_n, ldx_t, N, t, i, w_hh, h0, out, ldo_n, ldo_t, gates, dout, ldd_n, ldd_t, dh_n, dh0, dgi, part); break;
+  }
+  if (rc != SLDM_OK) return rc;
+  const int64_t stride = 3 * H * H + 3 * H * 16 + 4 * H;
+  gru_reduce_kernel<<<(unsigned)((stride + 255) / 256), 256, 0, st>>>(
+      part, tiles, (int)H, i, dw_ih, dw_hh, db_ih, db_hh);
+  SLDM_LAUNCH_CHECK("gru_reduce_kernel");
+  if (dx) {
+    const int64_t rows = N * T;
+    gru_dx_kernel<<<(unsigned)((rows * I + 255) / 256), 256, 0, st>>>(dgi, w_ih, rows, (int)H,
+                                                                       i, dx, T, lddx_n, lddx_t);
+    SLDM_LAUNCH_CHECK("gru_dx_kernel");
+  }
+  return SLDM_OK;
+}

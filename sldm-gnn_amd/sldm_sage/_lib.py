@@ -15,7 +15,7 @@ import torch  # noqa: F401  (must be imported before the HIP library)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SLDM_SAGE_LIB", os.path.join(_HERE, "libsldm_sage.so"))
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 F32, BF16 = 0, 1
 
 _c_i64 = ctypes.c_int64
@@ -80,6 +80,15 @@ _SIGNATURES = {
     "sldm_radius_edges": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _c_i64,
                                          _c_i64, _c_i64, ctypes.c_float, _vp, _c_i64, _vp, _vp,
                                          _vp, ctypes.c_size_t, _vp]),
+    "sldm_gru_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, _c_i64]),
+    "sldm_gru_fwd": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _vp,
+                                    _vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp]),
+    "sldm_gru_bwd_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, _c_i64, _c_i64,
+                                                       ctypes.c_int]),
+    "sldm_gru_bwd": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _vp,
+                                    _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_i64, _c_i64,
+                                    _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                    ctypes.c_size_t, _vp]),
 }
 
 _lock = threading.Lock()

@@ -224,3 +224,35 @@ def test_bf16_oracle_rounds_where_stored():
     s = out32.abs().max()
     assert (out - out32).abs().max() < 2e-2 * s
     assert 0 < branch_margin(block_params(ref), x, ei, 0.1) < 1e-2
+
+
+# --------------------------------------------------------------- GRU oracle --
+@pytest.mark.parametrize("batch_first,bias,h0", [(True, True, False), (False, True, True),
+                                                 (True, False, True)])
+def test_gru_oracle_matches_torch_gru(batch_first, bias, h0):
+    """oracle/gru_ref.py (aten's GRU cell unrolled) equals torch.nn.GRU on CPU,
+    forward and every gradient (the reference's own op, grusage.py:66-71)."""
+    from oracle.gru_ref import gru_ref
+    torch.manual_seed(0)
+    N, T, I, H = 7, 9, 6, 16
+    gru = torch.nn.GRU(I, H, 1, bias=bias, batch_first=batch_first)
+    x = torch.randn((N, T, I) if batch_first else (T, N, I), requires_grad=True)
+    hx = torch.randn(1, N, H, requires_grad=True) if h0 else None
+    out, hn = gru(x, hx)
+    g1, g2 = torch.randn_like(out), torch.randn_like(hn)
+    (out * g1).sum().add((hn * g2).sum()).backward()
+    ref_grads = [p.grad.clone() for p in gru.parameters()] + [x.grad.clone()]
+    if h0:
+        ref_grads.append(hx.grad.clone())
+    params = [p.detach().clone().requires_grad_(True) for p in gru.parameters()]
+    x2 = x.detach().clone().requires_grad_(True)
+    hx2 = hx.detach().clone().requires_grad_(True) if h0 else None
+    w_ih, w_hh = params[0], params[1]
+    b_ih, b_hh = (params[2], params[3]) if bias else (None, None)
+    out2, hn2 = gru_ref(x2, w_ih, w_hh, b_ih, b_hh, hx2, batch_first)
+    (out2 * g1).sum().add((hn2 * g2).sum()).backward()
+    torch.testing.assert_close(out2, out, atol=1e-6, rtol=1e-5)
+    torch.testing.assert_close(hn2, hn, atol=1e-6, rtol=1e-5)
+    got = [p.grad for p in params] + [x2.grad] + ([hx2.grad] if h0 else [])
+    for a, b in zip(got, ref_grads):
+        torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)

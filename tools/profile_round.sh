@@ -20,7 +20,7 @@ i=0
 for ctr in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i + 1))
   timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc_${R}_$i" -o run \
-    -- python3 "$ROOT/tools/kbench.py" --only gather,dense,nt,tn,post --reps 1 \
+    -- python3 "$ROOT/tools/kbench.py" --only gather,dense,nt,tn,post,gpost --reps 1 \
     > "$OUT/pmc_${R}_$i.log" 2>&1 || { echo "pmc pass $i ($ctr) failed: $?"; exit 1; }
   echo "pmc pass $i ($ctr) ok"
 done
