@@ -59,7 +59,7 @@ class _GruFn(torch.autograd.Function):
                                                                         out.stride(0))
         h_n = torch.empty(1, N, H, dtype=torch.float32, device=dev)
         lib = _lib.load()
-        need = torch.is_grad_enabled() and any(ctx.needs_input_grad[:6])
+        need = any(ctx.needs_input_grad[:6])      # (grad mode is off inside forward)
         gates = None
         if need:
             gates = torch.empty(lib.sldm_gru_workspace_bytes(N, T, H) // 4,

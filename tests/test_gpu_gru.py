@@ -27,8 +27,8 @@ def _run_pair(N, T, I, H, batch_first=True, bias=True, h0=False, gout=True, gh=T
     gn = torch.randn(1, N, H, generator=g) if gh else None
 
     def run(mod, dev):
-        xx = x.to(dev).requires_grad_(dx)
-        hh = hx.to(dev).requires_grad_(True) if h0 else None
+        xx = x.detach().clone().to(dev).requires_grad_(dx)
+        hh = hx.detach().clone().to(dev).requires_grad_(True) if h0 else None
         out, hn = mod(xx, hh)
         loss = 0
         if go is not None:
