@@ -158,10 +158,28 @@ def cpu_baseline(cfg, threads, frac=10, budget_s=30.0):
         if time.perf_counter() > t_end and len(times) >= 1:
             break
     t = statistics.median(times)
+    # the framework's own host path on the same sample (SageBlock on CPU
+    # tensors: libsldm_sage_cpu.so + BLAS), beside the reference's op sequence
+    from sldm_sage import SageBlock
+    ours = SageBlock([f] * (L + 1), dropout=0.25, negative_slope=0.1)
+    ours.load_state_dict(blk.state_dict())
+    ours.train()
+    t_ours = []
+    for it in range(4):
+        xr = x.clone().requires_grad_(True)
+        ours.zero_grad(set_to_none=True)
+        t0 = time.perf_counter()
+        ours(xr, ei).backward(gout)
+        if it > 0:
+            t_ours.append(time.perf_counter() - t0)
+    to = statistics.median(t_ours)
     return dict(value=es * L / t, unit="edges/s", cores=threads, kind="port",
                 sample=f"{ns} nodes / {es} edges (1/{frac} of the workload), F={f}, L={L}, fp32, "
                        f"median of {len(times)} fwd+bwd after 1 warm-up; oracle/sage_ref.py",
-                ms_per_step=t * 1e3)
+                ms_per_step=t * 1e3,
+                sldm_cpu_path={"value": es * L / to, "ms_per_step": to * 1e3,
+                               "note": "sldm_sage.SageBlock on CPU tensors (native host "
+                                       "kernels + BLAS), same sample and threads, median of 3"})
 
 
 # ---------------------------------------------------------------------------

@@ -91,8 +91,14 @@ def build_graph(edge_index: torch.Tensor, num_nodes: int, transpose: bool = True
     maximum degrees in the same sync (and a skewed one a second time, for
     the hub plan's size).
     """
-    rowptr, col, t_rowptr, t_col, bad = ops.csr_build(edge_index, num_nodes, transpose)
     E = int(edge_index.size(1))
+    if edge_index.device.type == "cpu":
+        # the reference's CPU mode (main.py:58): host kernels (cpu.py), which
+        # validate the ids as they count
+        from . import cpu
+        rowptr, col, t_rowptr, t_col = cpu.csr_build(edge_index, num_nodes, transpose)
+        return SageGraph(num_nodes, E, rowptr, col, t_rowptr, t_col)
+    rowptr, col, t_rowptr, t_col, bad = ops.csr_build(edge_index, num_nodes, transpose)
     g = SageGraph(num_nodes, E, rowptr, col, t_rowptr, t_col)
     mode = _skew_mode()
     skew_check = E >= HUB_MIN_EDGES and num_nodes > 0 and mode != "none"

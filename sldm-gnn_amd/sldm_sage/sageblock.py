@@ -307,6 +307,8 @@ class SageBlock(nn.Module):
             return x
         if x.dim() != 2:
             raise ValueError(f"SageBlock expects x [N, F], got {tuple(x.shape)}")
+        if x.device.type == "cpu":
+            return self._forward_cpu(x, edge_index)
         ops._require_gpu(x)
         grad = torch.is_grad_enabled() and (
             x.requires_grad or any(p.requires_grad for p in self.parameters()))
@@ -331,3 +333,32 @@ class SageBlock(nn.Module):
         for (wl, bl, wr, gamma, beta), (slope, p, seed, eps) in layers:
             x = _SageLayerFn.apply(x, wl, bl, wr, gamma, beta, graph, slope, p, seed, eps)
         return x
+
+    def _forward_cpu(self, x: torch.Tensor, edge_index) -> torch.Tensor:
+        """CPU tensors (the reference's DEVICE='cpu' mode): the host kernels of
+        cpu.py, fp32 (the reference's dtype), one autograd node per layer."""
+        from .cpu import _CpuLayerFn
+        if x.dtype != torch.float32:
+            raise TypeError(f"SageBlock on CPU computes in float32 (the reference's dtype), "
+                            f"got {x.dtype}")
+        if isinstance(edge_index, torch.Tensor) and edge_index.device.type != "cpu":
+            raise RuntimeError("SageBlock: x is on the CPU but edge_index is on "
+                               f"{edge_index.device}")
+        grad = torch.is_grad_enabled() and (
+            x.requires_grad or any(p.requires_grad for p in self.parameters()))
+        graph = get_graph(edge_index, x.size(0), transpose=grad)
+        x = x.contiguous()
+        for conv, post in zip(self.convs, self.posts):
+            ln, act, drop = post[0], post[1], post[2]
+            p = _drop_p(drop)
+            seed = _cpu_seed() if p > 0 else 0
+            x = _CpuLayerFn.apply(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight,
+                                  ln.weight, ln.bias, graph, _act_slope(act), p, seed,
+                                  float(ln.eps))
+        return x
+
+
+def _cpu_seed() -> int:
+    """Dropout key for a CPU-mode layer call, from torch's CPU generator (the
+    generator nn.Dropout on CPU draws from), so torch.manual_seed governs it."""
+    return int(torch.randint(0, 2**62, (1,)).item())

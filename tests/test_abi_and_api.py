@@ -63,10 +63,18 @@ def test_state_dict_layout_matches_reference():
             assert [type(m) for m in pa] == [type(m) for m in pb]
 
 
-def test_cpu_tensors_fail_loudly():
-    from sldm_sage import SageBlock
-    blk = SageBlock([4, 4], None, 0.1)
+def test_gpu_ops_have_no_cpu_fallback(monkeypatch):
+    """The GPU op layer rejects CPU tensors (no silent fallback); SageBlock sends
+    CPU tensors explicitly to the native host library, and raises if that
+    library is missing instead of falling back to torch."""
+    from sldm_sage import SageBlock, cpu, ops
     with pytest.raises(RuntimeError, match="no CPU fallback"):
+        ops.gather_rows(torch.randn(3, 4), torch.zeros(4, dtype=torch.int32),
+                        torch.zeros(0, dtype=torch.int32), 3, mean=True)
+    monkeypatch.setattr(cpu, "CPU_LIB_PATH", "/nonexistent/libsldm_sage_cpu.so")
+    monkeypatch.setattr(cpu, "_lib", None)
+    blk = SageBlock([4, 4], None, 0.1)
+    with pytest.raises(RuntimeError, match="libsldm_sage_cpu.so not found"):
         blk(torch.randn(3, 4), torch.tensor([[0, 1], [1, 2]]))
 
 
@@ -84,3 +92,16 @@ def test_dropin_module_importable():
     spec.loader.exec_module(mod)
     from sldm_sage import SageBlock
     assert mod.SageBlock is SageBlock
+
+
+def test_cpu_library_exports_header():
+    """libsldm_sage_cpu.so (CPU-tensor path) exports every symbol its header declares."""
+    from sldm_sage import cpu
+    hdr = open(os.path.join(ROOT, "include", "sldm_sage_cpu.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    declared = sorted(set(re.findall(r"\b(sldm_cpu_[a-z0-9_]+)\s*\(", hdr)))
+    lib = cpu.load()
+    assert len(declared) == 6
+    for name in declared:
+        assert hasattr(lib, name) and name in cpu.exported_symbols(), name
+    assert lib.sldm_cpu_abi_version() == 1

@@ -1206,3 +1206,19 @@ def test_dropout_seeds_leave_cpu_rng_untouched():
     assert not torch.equal(a, b)                      # fresh masks per call
     torch.manual_seed(5)
     assert torch.equal(blk(xg, eig), a)               # reproducible under manual_seed
+
+
+def test_cpu_and_gpu_dropout_masks_agree():
+    """The host library (CPU mode) regenerates the GPU kernels' dropout hash:
+    same (seed, row, column) -> same mask, so CPU and GPU runs are comparable."""
+    from sldm_sage import cpu, ops
+    n, f = 300, 96
+    h = torch.randn(n, f, generator=torch.Generator().manual_seed(3))
+    gam, bet = torch.ones(f), torch.zeros(f)
+    out_g, _, _ = ops.post_fwd(h.to(DEV), None, gam.to(DEV), bet.to(DEV), 1e-5, 0.1, 0.25,
+                               987654321, torch.float32, False, row_offset=5)
+    out_c = torch.empty(n, f)
+    cpu.load().sldm_cpu_post_fwd(h.data_ptr(), f, n, f, None, gam.data_ptr(), bet.data_ptr(),
+                                 1e-5, 0.1, 0.25, 987654321, 5, out_c.data_ptr(), None, None)
+    assert torch.equal(out_g.cpu() != 0, out_c != 0)
+    torch.testing.assert_close(out_g.cpu(), out_c, atol=1e-5, rtol=1e-5)
