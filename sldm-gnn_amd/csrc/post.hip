@@ -126,7 +126,10 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
   const uint32_t dthr = sldm::dropout_threshold(drop_p);
   // RB rows per thread group and iteration, all loads issued before the
   // first use (bytes in flight: this kernel is HBM-bound)
-  constexpr int RB = 2;
+#ifndef SLDM_POST_RB
+#define SLDM_POST_RB 2
+#endif
+  constexpr int RB = SLDM_POST_RB;
   const int64_t stride = (int64_t)gridDim.x * groups_per_block;
   const int64_t nrounds = (nrows + RB * stride - 1) / (RB * stride);
   for (int64_t it = 0; it < nrounds; ++it) {
