@@ -182,6 +182,50 @@ def cpu_baseline(cfg, threads, frac=10, budget_s=30.0):
                                        "kernels + BLAS), same sample and threads, median of 3"})
 
 
+def torch_ops_gpu_baseline(blk, ei, x, gout, warmup=1, steps=2):
+    """The reference's GPU path on this GPU: PyG 2.7.0 ``SAGEConv(mean)`` +
+    the SageBlock post stack (sageblock.py:16-20) as the ATen ops PyG issues --
+    ``index_select`` of the [E, F] messages, ``scatter_add_`` of messages and
+    of the fp32 count, ``clamp(min=1)``, division, ``lin_l`` + ``lin_r``,
+    LayerNorm, LeakyReLU, Dropout -- with ``blk``'s weights, in x's dtype,
+    fwd + bwd of the same upstream gradient.  A measurement baseline (the
+    framework never runs it); None if it does not fit in memory."""
+    import torch.nn.functional as Fn
+    src, dst = ei[0], ei[1]
+    n = x.size(0)
+    cv = dict(device=x.device, dtype=x.dtype)
+    layers = [tuple(t.detach().to(**cv).requires_grad_(True) for t in
+                    (c.lin_l.weight, c.lin_l.bias, c.lin_r.weight, p[0].weight, p[0].bias))
+              for c, p in zip(blk.convs, blk.posts)]
+
+    def step():
+        h = x.detach().requires_grad_(True)
+        for wl, bl, wr, g, b in layers:
+            xj = h.index_select(0, src)
+            cnt = torch.zeros(n, dtype=h.dtype, device=h.device).scatter_add_(
+                0, dst, torch.ones(dst.numel(), dtype=h.dtype, device=h.device)).clamp(min=1)
+            agg = torch.zeros(n, h.size(1), dtype=h.dtype, device=h.device).scatter_add_(
+                0, dst.view(-1, 1).expand_as(xj), xj) / cnt.view(-1, 1)
+            o = Fn.linear(agg, wl, bl) + Fn.linear(h, wr)
+            o = Fn.layer_norm(o, (o.size(1),), g, b, 1e-5)
+            h = Fn.dropout(Fn.leaky_relu(o, 0.1), 0.25, training=True)
+        h.backward(gout)
+
+    try:
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps
+    except torch.cuda.OutOfMemoryError:
+        return None
+    finally:
+        torch.cuda.empty_cache()
+
+
 # ---------------------------------------------------------------------------
 # Real-workload lines (VERDICT r1 "what's missing" 5; SURVEY §7 hard part (iv))
 # ---------------------------------------------------------------------------
@@ -244,6 +288,15 @@ def bench_vehicle(args, dev):
         out.backward(torch.ones_like(out))
 
     t = _time_steps(step, args.warmup, args.steps)
+    # the reference's ATen op sequence on the same batches (what PyG runs)
+    t_ref = []
+    for pool in pools[:4]:
+        b = collate([dict(p) for p in pool])
+        tb = torch_ops_gpu_baseline(blk, b.edge_index, b.h, torch.ones(b.h.size(0), hd[-1],
+                                                                       device=dev),
+                                    warmup=2, steps=5)
+        if tb:
+            t_ref.append(tb)
     e_avg, n_avg = sum(edges) / len(edges), sum(nodes) / len(nodes)
     return {"metric": "edges/sec SageBlock fwd+bwd (vehicle batches)", "value": round(
         e_avg * (len(hd) - 1) / t, 1), "unit": "edges/s", "n_gpus": 1, "steps": args.steps,
@@ -253,7 +306,11 @@ def bench_vehicle(args, dev):
         "config": {"workload": "vehicle SageBlock [128,96,96], 32 packs / batch incl. collate + "
                                "per-batch CSR", "nodes_per_batch": round(n_avg),
                    "edges_per_batch": round(e_avg), "dropout": 0.25, "negative_slope": 0.1},
-        "graphs_per_s": round(PACKS_PER_BATCH / t, 1)}
+        "graphs_per_s": round(PACKS_PER_BATCH / t, 1),
+        "torch_ops_gpu_baseline": ({"ms_per_step": round(statistics.median(t_ref) * 1e3, 3),
+                                    "note": "reference ATen op sequence on the same batches "
+                                            "(collate and CSR not included)"}
+                                   if t_ref else None)}
 
 
 def bench_map(args, dev):
@@ -356,6 +413,8 @@ def main():
                          "(per-batch small graphs, grusage.py:108 / mapencoder.py:18-25) or gru "
                          "(the model's GRU, grusage.py:160-161)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-torch-baseline", action="store_true",
+                    help="skip timing the reference's ATen op sequence on the GPU")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="host threads of the CPU baseline (default: every usable CPU)")
     ap.add_argument("--cpu-frac", type=int, default=10,
@@ -568,6 +627,22 @@ def main():
     kernels = {k: dict(avg_ms=round(v["avg_ms"], 4), launches=v["launches"],
                        gbs=round(v["avg_bytes"] / (v["avg_ms"] * 1e-3) / 1e9, 1))
                for k, v in kern.items()}
+    torch_gpu = None
+    if world == 1 and not use_dist and not args.no_torch_baseline:
+        ei_b, x_b = make_graph(n, e, f, dtype, dev, kind=args.graph)
+        torch.manual_seed(0)
+        blk_b = SageBlock([f] * (L + 1), dropout=0.25, negative_slope=0.1)
+        g_b = torch.randn(n, f, device=dev, generator=torch.Generator(device=dev).manual_seed(2)
+                          ).to(dtype)
+        t_b = torch_ops_gpu_baseline(blk_b, ei_b, x_b, g_b)
+        del ei_b, x_b, g_b
+        torch.cuda.empty_cache()
+        torch_gpu = ({"value": round(e * L / t_b, 1), "ms_per_step": round(t_b * 1e3, 3),
+                      "speedup": round(t_b / (elapsed / args.steps), 2),
+                      "what": "the reference's ATen op sequence (PyG 2.7.0 SAGEConv(mean): "
+                              "index_select + scatter_add_ + count + linear; LayerNorm, "
+                              "LeakyReLU, Dropout) on this GPU, same graph / dtype / weights"}
+                     if t_b else {"value": None, "note": "out of memory at this size"})
     if rank == 0:
         base = None
         if world == 1 and not args.no_cpu_baseline:
@@ -601,6 +676,7 @@ def main():
             "roofline": roof,
             "kernels": kernels,
             "cpu_baseline": base,
+            "torch_ops_gpu_baseline": torch_gpu,
         }
         if variant is not None:
             line["locality_variant"] = variant
