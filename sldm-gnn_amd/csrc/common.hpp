@@ -276,6 +276,7 @@ int stream_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, i
 // gemm_ws.hip: weight-stationary dX kernel (weights in VGPRs, LDS-DMA tiles).
 bool ws_gemm_enabled();
 bool ws_fwd_enabled();
+int ws_fwd_mode();
 // gemm_tn_dma.hip: row-streaming dW kernel (LDS-DMA, transposed reads).
 bool tn_dma_enabled();
 bool tn_dma_ok(int64_t mo, int64_t n0, int64_t n1, int64_t rows, const void* a, int64_t lda,

@@ -250,12 +250,21 @@ struct WsLnArgs {
   float eps, slope, drop_p, drop_scale; uint64_t seed; int64_t row_off;
 };
 
-template <int KSTEPS, int NBUF, int TM>
+// XCHG selects the epilogue: false re-distributes z through LDS so one wave
+// owns whole rows ([TM][256] fp32 staging); true keeps z in the MFMA layout and
+// exchanges only the per-row LayerNorm partial sums (2 x [TM][8] fp32).
+#ifndef SLDM_WSLN_PF
+#define SLDM_WSLN_PF 2
+#endif
+constexpr int WSLN_PF = SLDM_WSLN_PF;
+
+template <int KSTEPS, int NBUF, int TM, bool XCHG>
 constexpr size_t ws_ln_lds_bytes() {
-  return (size_t)NBUF * TM * KSTEPS * 64 + 3 * 256 * sizeof(float) + (size_t)TM * 1024;
+  return (size_t)NBUF * TM * KSTEPS * 64 + 3 * 256 * sizeof(float) +
+         (XCHG ? (size_t)2 * TM * 8 * sizeof(float) : (size_t)TM * 1024);
 }
 
-template <int KSTEPS, int K0STEPS, int NBUF, int TM>
+template <int KSTEPS, int K0STEPS, int NBUF, int TM, bool XCHG>
 __global__ __launch_bounds__(kThreads) void ws_ln_kernel(WsLnArgs p) {
   constexpr int CT = 2;
   constexpr int K1STEPS = KSTEPS - K0STEPS;
@@ -380,7 +389,9 @@ __global__ __launch_bounds__(kThreads) void ws_ln_kernel(WsLnArgs p) {
       lb0[b] = sl + (uint32_t)(i * RB0) + o;
       lb1[b] = sl + (uint32_t)(SUB1 + i * RB1) + o;
     }
-    s8v bf[2][RG];
+    // B fragments PF k-steps ahead (PF = 1 for the z-redistributing epilogue)
+    constexpr int PF = XCHG ? WSLN_PF : 1;
+    s8v bf[PF + 1][RG];
     auto read_b = [&](int s, s8v (&dst)[RG]) {
       const bool s1 = s >= K0STEPS;
       const int ls = s1 ? s - K0STEPS : s;
@@ -389,18 +400,123 @@ __global__ __launch_bounds__(kThreads) void ws_ln_kernel(WsLnArgs p) {
 #pragma unroll
       for (int m = 0; m < RG; ++m) dst[m] = *(lds_frag)(uintptr_t)(a + (uint32_t)(16 * m * rb));
     };
-    read_b(0, bf[0]);
+#pragma unroll
+    for (int s = 0; s < PF; ++s) read_b(s, bf[s]);
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
-      if (s + 1 < KSTEPS) read_b(s + 1, bf[(s + 1) & 1]);
+      if (s + PF < KSTEPS) read_b(s + PF, bf[(s + PF) % (PF + 1)]);
 #pragma unroll
       for (int m = 0; m < RG; ++m)
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
-          acc[m][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ct][s], bf[s & 1][m], acc[m][ct],
-                                                              0, 0, 0);
-      if (s + 1 < KSTEPS) __builtin_amdgcn_sched_group_barrier(0x100, RG, 0);
+          acc[m][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ct][s], bf[s % (PF + 1)][m],
+                                                              acc[m][ct], 0, 0, 0);
+      if (s + PF < KSTEPS) __builtin_amdgcn_sched_group_barrier(0x100, RG, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, RG * CT, 0);
+    }
+
+    if constexpr (XCHG) {
+      // ---- epilogue, exchange form: acc[m][ct][r] = z[row 16m + i][col
+      // cbase + 16ct + 4q + r] stays in place.  Row sums: in-lane over the
+      // lane's 8 columns, then over the 4 lanes of the row (q, xor 16 / 32),
+      // then the 8 waves' partials through LDS (red[row][wave], summed in wave
+      // order after a barrier); the same for the squared deviations.  Two
+      // buffers, so tile n+1's first exchange never races tile n's reads (every
+      // wave has read buffer 0 before it reaches the second barrier).
+      float* red = reinterpret_cast<float*>(zs);
+      auto row_total = [&](float (&part)[RG], int buf, float (&tot)[RG]) {
+#pragma unroll
+        for (int m = 0; m < RG; ++m) {
+          float v = part[m];
+          v += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F));
+          v += __shfl_xor(v, 32, 64);
+          if (q == 0) red[(buf * TM + 16 * m + i) * 8 + wave] = v;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+        for (int m = 0; m < RG; ++m) {
+          const f4v* pr = reinterpret_cast<const f4v*>(red + (buf * TM + 16 * m + i) * 8);
+          const f4v a = pr[0], b = pr[1];
+          tot[m] = a[0] + a[1] + a[2] + a[3] + b[0] + b[1] + b[2] + b[3];
+        }
+      };
+      float part[RG], tot[RG];
+#pragma unroll
+      for (int m = 0; m < RG; ++m) {
+        part[m] = 0.f;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const f4v bb = *reinterpret_cast<const f4v*>(prm + cbase + 16 * ct + 4 * q);
+          acc[m][ct] += bb;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) part[m] += acc[m][ct][r];
+        }
+      }
+      row_total(part, 0, tot);
+#pragma unroll
+      for (int m = 0; m < RG; ++m) {
+        const float mean = tot[m] * inv_n;
+        part[m] = 0.f;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float d = acc[m][ct][r] - mean;
+            acc[m][ct][r] = d;
+            part[m] += d * d;
+          }
+      }
+      row_total(part, 1, tot);
+      const int64_t r0 = tile * TM;
+      const int ccol = cbase + ((q & 1) ? 16 + 4 * (q - 1) : 4 * q);
+      float rs[RG];
+#pragma unroll
+      for (int m = 0; m < RG; ++m) {
+        rs[m] = 1.0f / sqrtf(tot[m] * inv_n + p.eps);
+        // rows past M hold row M-1's (clamped) activations and rewrite row M-1
+        const int64_t row = r0 + 16 * m + i < p.M ? r0 + 16 * m + i : p.M - 1;
+        const uint32_t rkey = sldm::dropout_row_key(p.seed, (uint64_t)(row + p.row_off));
+        uint32_t wx[CT][2], wo[CT][2];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const int c = cbase + 16 * ct + 4 * q;
+          const f4v gg = *reinterpret_cast<const f4v*>(prm + 256 + c);
+          const f4v be = *reinterpret_cast<const f4v*>(prm + 512 + c);
+          bool keep[4] = {true, true, true, true};
+          if (p.drop_p > 0.f) {
+            sldm::dropout_keep2(rkey, (uint32_t)c, dthr, keep[0], keep[1]);
+            sldm::dropout_keep2(rkey, (uint32_t)c + 2, dthr, keep[2], keep[3]);
+          }
+          float xh[4], o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            xh[r] = acc[m][ct][r] * rs[m];
+            const float y = xh[r] * gg[r] + be[r];
+            const float a = y > 0.f ? y : y * p.slope;
+            o[r] = keep[r] ? a * p.drop_scale : 0.f;
+          }
+          wx[ct][0] = sldm::pack_bf16x2(xh[0], xh[1]);
+          wx[ct][1] = sldm::pack_bf16x2(xh[2], xh[3]);
+          wo[ct][0] = sldm::pack_bf16x2(o[0], o[1]);
+          wo[ct][1] = sldm::pack_bf16x2(o[2], o[3]);
+        }
+        // tiles 0 and 1 leave together, one 16-B store per lane (ws_rowscale)
+        if (hasx) {
+          auto s0 = __builtin_amdgcn_permlane16_swap(wx[0][0], wx[1][0], false, false);
+          auto s1 = __builtin_amdgcn_permlane16_swap(wx[0][1], wx[1][1], false, false);
+          *reinterpret_cast<uint4*>(p.xhat + row * 256 + ccol) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        }
+        auto s0 = __builtin_amdgcn_permlane16_swap(wo[0][0], wo[1][0], false, false);
+        auto s1 = __builtin_amdgcn_permlane16_swap(wo[0][1], wo[1][1], false, false);
+        *reinterpret_cast<uint4*>(p.out + row * 256 + ccol) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      }
+      // rstd: one store per wave (the same count in every wave, for vmcnt):
+      // lane l < 16 holds row l in rs[0], lane 16 + l row 16 + l in rs[1]
+      if (p.rstd && lane < 32) {
+        const int64_t row = r0 + lane < p.M ? r0 + lane : p.M - 1;
+        p.rstd[row] = lane < 16 ? rs[0] : rs[1];
+      }
+      continue;
     }
 
     // ---- epilogue, row-owner form: the MFMA layout spreads a row over all 8
@@ -505,13 +621,13 @@ int launch_ws(WsArgs& p, hipStream_t stream) {
   return SLDM_OK;
 }
 
-template <int KSTEPS, int K0STEPS, int NBUF, int TM>
+template <int KSTEPS, int K0STEPS, int NBUF, int TM, bool XCHG>
 int launch_ws_ln(WsLnArgs& p, hipStream_t stream) {
-  constexpr size_t lds = ws_ln_lds_bytes<KSTEPS, NBUF, TM>();
+  constexpr size_t lds = ws_ln_lds_bytes<KSTEPS, NBUF, TM, XCHG>();
   static_assert(lds <= 160 * 1024, "LDS budget");
   p.ntiles = (p.M + TM - 1) / TM;
   const int64_t grid = std::min<int64_t>(p.ntiles, num_cus());
-  auto kern = ws_ln_kernel<KSTEPS, K0STEPS, NBUF, TM>;
+  auto kern = ws_ln_kernel<KSTEPS, K0STEPS, NBUF, TM, XCHG>;
   SLDM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   kern<<<(unsigned)grid, kThreads, lds, stream>>>(p);
@@ -535,10 +651,13 @@ bool ws_gemm_enabled() {
 // dropout row key, addressing) is repeated by 32 lanes instead of 4, ~55 VALU
 // instructions per output element against the stream kernel's ~15, and it
 // measured 5.4-5.6 ms against 4.8 at C4.
-bool ws_fwd_enabled() {
+// SLDM_WS_FWD=2 selects the statistics-exchange epilogue (no z round trip).
+int ws_fwd_mode() {
   const char* e = getenv("SLDM_WS_FWD");
-  return ws_gemm_enabled() && e && e[0] == '1';
+  if (!ws_gemm_enabled() || !e) return 0;
+  return e[0] == '1' ? 1 : (e[0] == '2' ? 2 : 0);
 }
+bool ws_fwd_enabled() { return ws_fwd_mode() != 0; }
 
 // Shape gate: bf16 (caller), K = 256, Nc = 512 (CT = 4) or 256 (CT = 2),
 // 16-B aligned rows and bases; a split / scaled boundary on a wave's column
@@ -598,14 +717,24 @@ int ws_dense_fwd(const void* a0, int64_t lda0, int64_t k0, const void* a1, int64
   p.drop_scale = drop_p >= 1.f ? 0.f : (drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f);
   p.seed = seed; p.row_off = row_off;
   const int64_t K = k0 + k1;
-  if (K == 512) {
-    if (k0 == 256) return launch_ws_ln<16, 8, 3, 32>(p, stream);
-    if (k0 == 128) return launch_ws_ln<16, 4, 3, 32>(p, stream);
-    if (k0 == 384) return launch_ws_ln<16, 12, 3, 32>(p, stream);
-    return launch_ws_ln<16, 16, 3, 32>(p, stream);
+  if (ws_fwd_mode() == 1) {
+    if (K == 512) {
+      if (k0 == 256) return launch_ws_ln<16, 8, 3, 32, false>(p, stream);
+      if (k0 == 128) return launch_ws_ln<16, 4, 3, 32, false>(p, stream);
+      if (k0 == 384) return launch_ws_ln<16, 12, 3, 32, false>(p, stream);
+      return launch_ws_ln<16, 16, 3, 32, false>(p, stream);
+    }
+    if (k0 == 128) return launch_ws_ln<8, 4, 4, 32, false>(p, stream);
+    return launch_ws_ln<8, 8, 4, 32, false>(p, stream);
   }
-  if (k0 == 128) return launch_ws_ln<8, 4, 4, 32>(p, stream);
-  return launch_ws_ln<8, 8, 4, 32>(p, stream);
+  if (K == 512) {
+    if (k0 == 256) return launch_ws_ln<16, 8, 4, 32, true>(p, stream);
+    if (k0 == 128) return launch_ws_ln<16, 4, 4, 32, true>(p, stream);
+    if (k0 == 384) return launch_ws_ln<16, 12, 4, 32, true>(p, stream);
+    return launch_ws_ln<16, 16, 4, 32, true>(p, stream);
+  }
+  if (k0 == 128) return launch_ws_ln<8, 4, 8, 32, true>(p, stream);
+  return launch_ws_ln<8, 8, 8, 32, true>(p, stream);
 }
 
 }  // namespace sldm

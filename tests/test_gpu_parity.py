@@ -658,11 +658,12 @@ STREAM_ROWS = [1, 255, 256, 257, 2000, 70_001]
 
 @pytest.mark.parametrize("m", STREAM_ROWS + [63, 65])
 @pytest.mark.parametrize("fi", [128, 256])
-@pytest.mark.parametrize("kernel", ["ws", "stream"])
+@pytest.mark.parametrize("kernel", ["ws", "ws_xchg", "stream"])
 def test_stream_dense_fwd_vs_torch_and_mask(m, fi, kernel, monkeypatch):
-    """Both bf16 forward kernels: gemm_ws.hip (weights in VGPRs, LayerNorm
-    statistics reduced across the 8 waves through LDS) and gemm_stream.hip."""
-    monkeypatch.setenv("SLDM_WS_FWD", "1" if kernel == "ws" else "0")
+    """The bf16 forward kernels: gemm_ws.hip (weights in VGPRs; z re-distributed
+    through LDS, or only the LayerNorm partial sums exchanged across the 8
+    waves) and gemm_stream.hip."""
+    monkeypatch.setenv("SLDM_WS_FWD", {"ws": "1", "ws_xchg": "2", "stream": "0"}[kernel])
     from sldm_sage import ops
     from sldm_sage.dense import weight_cat
     fo, p, seed = 256, 0.25, 4242
@@ -718,10 +719,12 @@ def test_tn_dma_weight_grad_vs_torch(rows, n1, monkeypatch):
 
 @pytest.mark.parametrize("m", [1, 65, 4097, 130_000])
 @pytest.mark.parametrize("k0,k1", [(256, 256), (128, 128), (256, 0), (512, 0), (128, 384)])
-def test_ws_dense_fwd_matches_stream(m, k0, k1, monkeypatch):
-    """The opt-in weight-stationary forward (SLDM_WS_FWD=1) and the default
-    kernel differ only in the LayerNorm statistics' fp32 summation order:
-    same dropout mask, outputs within one bf16 rounding."""
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_ws_dense_fwd_matches_stream(m, k0, k1, mode, monkeypatch):
+    """The weight-stationary forwards (SLDM_WS_FWD=1: z re-distributed through
+    LDS; 2: LayerNorm partial sums exchanged) and the stream kernel differ only
+    in the LayerNorm statistics' fp32 summation order: same dropout mask,
+    outputs within one bf16 rounding."""
     from sldm_sage import ops
     gen = torch.Generator(device=DEV).manual_seed(m + k0)
     a0 = torch.randn(m, k0, generator=gen, device=DEV).bfloat16()
@@ -731,7 +734,7 @@ def test_ws_dense_fwd_matches_stream(m, k0, k1, monkeypatch):
     be = torch.full((256,), 5.0, device=DEV)
 
     def run(ws):
-        monkeypatch.setenv("SLDM_WS_FWD", "1" if ws else "0")
+        monkeypatch.setenv("SLDM_WS_FWD", mode if ws else "0")
         out = torch.empty(m, 256, dtype=torch.bfloat16, device=DEV)
         xh = torch.empty_like(out)
         rs = torch.empty(m, device=DEV)

@@ -79,11 +79,13 @@ def main():
                                                    save), a.reps)
             add(f"dense_fwd p={p_} save={save}", ms, (2 * n * f + n * f * (2 if save else 1)) * s,
                 fl)
-        for var, env in [("ws", {"SLDM_WS_FWD": "1"})]:
+        for var, env, p_ in [("ws", {"SLDM_WS_FWD": "1"}, 0.25),
+                             ("ws_xchg", {"SLDM_WS_FWD": "2"}, 0.25),
+                             ("ws_xchg", {"SLDM_WS_FWD": "2"}, 0.0)]:
             os.environ.update(env)
-            ms = timeit(lambda: ops.sage_dense_fwd(agg, x, wcat, b, gam, bet, 1e-5, 0.1, 0.25, 7,
+            ms = timeit(lambda: ops.sage_dense_fwd(agg, x, wcat, b, gam, bet, 1e-5, 0.1, p_, 7,
                                                    True), a.reps)
-            add(f"dense_fwd p=0.25 save=True {var}", ms, 4 * n * f * s, fl)
+            add(f"dense_fwd p={p_} save=True {var}", ms, 4 * n * f * s, fl)
             for k in env:
                 os.environ.pop(k)
     if want("nt"):
