@@ -199,6 +199,8 @@ def torch_ops_gpu_baseline(blk, ei, x, gout, warmup=1, steps=2):
               for c, p in zip(blk.convs, blk.posts)]
 
     def step():
+        for t in (t for lay in layers for t in lay):
+            t.grad = None                   # as a training loop's zero_grad(set_to_none)
         h = x.detach().requires_grad_(True)
         for wl, bl, wr, g, b in layers:
             xj = h.index_select(0, src)
@@ -243,7 +245,7 @@ def _synthetic_pack(gen, dev, v, feat, radius=30.0, strip=(600.0, 40.0)):
     adj = (d <= radius) & ~torch.eye(v, dtype=torch.bool, device=dev)
     ei = adj.nonzero().t().contiguous()          # i-major like gbuilder.py:92-109
     h = torch.randn(v, feat, generator=gen, device=dev)
-    return {"h": h, "edge_index": ei}
+    return {"x": h, "edge_index": ei}
 
 
 def _time_steps(step, warmup, steps):
@@ -262,8 +264,9 @@ def bench_vehicle(args, dev):
     context; main.py:39-46 dropout 0.25, slope 0.1) on collated batches of 32
     packs (main.py:166-167).  Packs are resident on the GPU (dataset.py:77
     loads with map_location=DEVICE); a step = PyG-free collate of 32 fresh
-    pack records (concat + edge_index offsets, sldm_sage.data.collate) + the
-    per-batch CSR build + SageBlock forward + backward.  8 batches rotate."""
+    pack records (sldm_sage.data.collate: feature concat + one fused kernel for
+    the offset edge_index, batch / ptr and the batch CSR pair, with one host
+    sync for the id check) + SageBlock forward + backward.  8 batches rotate."""
     from sldm_sage import SageBlock
     from sldm_sage.data import collate
     gen = torch.Generator(device=dev).manual_seed(0)
@@ -277,24 +280,32 @@ def bench_vehicle(args, dev):
     blk = SageBlock(hd, dropout=0.25, negative_slope=0.1).to(dev).train()
     it = [0]
     edges = [sum(p["edge_index"].size(1) for p in pool) for pool in pools]
-    nodes = [sum(p["h"].size(0) for p in pool) for pool in pools]
+    nodes = [sum(p["x"].size(0) for p in pool) for pool in pools]
 
     def step():
         pool = pools[it[0] % len(pools)]
         it[0] += 1
         b = collate([dict(p) for p in pool])          # fresh records: no cached CSR
-        h = b.h.requires_grad_(True)
+        blk.zero_grad(set_to_none=True)                # as a training loop does
+        h = b.x.requires_grad_(True)
         out = blk(h, b.edge_index)
         out.backward(torch.ones_like(out))
 
     t = _time_steps(step, args.warmup, args.steps)
-    # the reference's ATen op sequence on the same batches (what PyG runs)
-    t_ref = []
+    # Like for like on collated batches: the SageBlock forward + backward alone
+    # (batch CSR from collate) and the reference's ATen op sequence (what PyG
+    # runs on the batch's edge_index) on the same batches.
+    t_ref, t_own = [], []
     for pool in pools[:4]:
         b = collate([dict(p) for p in pool])
-        tb = torch_ops_gpu_baseline(blk, b.edge_index, b.h, torch.ones(b.h.size(0), hd[-1],
-                                                                       device=dev),
-                                    warmup=2, steps=5)
+        gout = torch.ones(b.x.size(0), hd[-1], device=dev)
+
+        def own(b=b, gout=gout):
+            blk.zero_grad(set_to_none=True)
+            blk(b.x.detach().requires_grad_(True), b.edge_index).backward(gout)
+
+        t_own.append(_time_steps(own, 2, 10))
+        tb = torch_ops_gpu_baseline(blk, b.edge_index, b.x, gout, warmup=2, steps=10)
         if tb:
             t_ref.append(tb)
     e_avg, n_avg = sum(edges) / len(edges), sum(nodes) / len(nodes)
@@ -304,12 +315,16 @@ def bench_vehicle(args, dev):
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic packs: 200-300 vehicles, 30 m radius graph in a 600x40 m strip",
         "config": {"workload": "vehicle SageBlock [128,96,96], 32 packs / batch incl. collate + "
-                               "per-batch CSR", "nodes_per_batch": round(n_avg),
+                               "batch CSR", "nodes_per_batch": round(n_avg),
                    "edges_per_batch": round(e_avg), "dropout": 0.25, "negative_slope": 0.1},
         "graphs_per_s": round(PACKS_PER_BATCH / t, 1),
+        "sageblock_only_ms": round(statistics.median(t_own) * 1e3, 3),
         "torch_ops_gpu_baseline": ({"ms_per_step": round(statistics.median(t_ref) * 1e3, 3),
-                                    "note": "reference ATen op sequence on the same batches "
-                                            "(collate and CSR not included)"}
+                                    "speedup_vs_sageblock_only": round(
+                                        statistics.median(t_ref) / statistics.median(t_own), 2),
+                                    "note": "reference ATen op sequence on the same collated "
+                                            "batches (collate not included; compare with "
+                                            "sageblock_only_ms)"}
                                    if t_ref else None)}
 
 
@@ -333,6 +348,7 @@ def bench_map(args, dev):
     blk = SageBlock([16, 32, 32], dropout=0.25, negative_slope=0.1).to(dev).train()
 
     def step():
+        blk.zero_grad(set_to_none=True)
         xr = x.detach().requires_grad_(True)
         out = blk(xr, ei)
         out.backward(torch.ones_like(out))

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SLDM_ABI_VERSION 4
+#define SLDM_ABI_VERSION 5
 
 enum sldm_dtype { SLDM_F32 = 0, SLDM_BF16 = 1 };
 enum sldm_status { SLDM_OK = 0, SLDM_ERR_ARG = 1, SLDM_ERR_HIP = 2 };
@@ -269,6 +269,28 @@ int sldm_radius_edges(const float* pos, int64_t pos_sv, int64_t pos_st, int64_t 
                       int64_t* edge_index, int64_t capacity, float* edge_attr,
                       int32_t* num_edges, void* workspace, size_t workspace_bytes,
                       void* stream);
+
+/* ------------------------------------------------------------ batching ---
+ * Batch.from_data_list for the edge_index of G graphs resident on the device
+ * (replaces PyG's collate behind main.py:166-167 for the
+ * packs dataset.py:77 loads onto DEVICE), fused with the batch CSR pair:
+ *   out_edge_index [2, out_ld] int64: graph g's edges at columns
+ *     [E_<g, E_<g + E_g), ids + N_<g (PyG __inc__);
+ *   out_batch [N] int64 (graph id per node), out_ptr [G+1] int64 (N_<g);
+ *   rowptr/col (CSR by destination), t_rowptr/t_col (by source, nullable
+ *   together), int32, rows in original edge order -- identical to
+ *   sldm_csr_build on out_edge_index.
+ * edge_index / edge_row_stride / num_edges / num_nodes are HOST arrays of G
+ * entries (edge_index[g]: device pointer to int64 [2, stride], row 1 at
+ * + stride).  bad_index_flag (device int32) is zeroed, then set to 1 if an id
+ * lies outside [0, N_g) of its graph (those edges are left out of the CSR; the
+ * caller raises).  N_g <= sldm_batch_graphs_max_nodes(). */
+int sldm_batch_graphs_max_nodes(void);
+int sldm_batch_graphs(int64_t num_graphs, const int64_t* const* edge_index,
+                      const int64_t* edge_row_stride, const int64_t* num_edges,
+                      const int64_t* num_nodes, int64_t* out_edge_index, int64_t out_ld,
+                      int64_t* out_batch, int64_t* out_ptr, int32_t* rowptr, int32_t* col,
+                      int32_t* t_rowptr, int32_t* t_col, int32_t* bad_index_flag, void* stream);
 
 /* ------------------------------------------------------------------- GRU ---
  * The model's trajectory GRU: torch.nn.GRU(I -> H,

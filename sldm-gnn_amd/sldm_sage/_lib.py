@@ -15,7 +15,7 @@ import torch  # noqa: F401  (must be imported before the HIP library)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SLDM_SAGE_LIB", os.path.join(_HERE, "libsldm_sage.so"))
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 F32, BF16 = 0, 1
 
 _c_i64 = ctypes.c_int64
@@ -76,6 +76,9 @@ _SIGNATURES = {
     "sldm_segment_pool_bwd": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _vp, _vp, _c_i64, _c_i64,
                                              _vp, _c_i64, _vp, _c_i64, _vp, _c_i64, _vp, _vp,
                                              _vp, _c_i64, _vp]),
+    "sldm_batch_graphs_max_nodes": (ctypes.c_int, []),
+    "sldm_batch_graphs": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp,
+                                         _vp, _vp, _vp, _vp, _vp]),
     "sldm_radius_edges_workspace_bytes": (ctypes.c_size_t, [_c_i64]),
     "sldm_radius_edges": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _c_i64,
                                          _c_i64, _c_i64, ctypes.c_float, _vp, _c_i64, _vp, _vp,

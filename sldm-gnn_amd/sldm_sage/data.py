@@ -112,10 +112,11 @@ class GraphBatch:
     ``batch.edge_index``, ``batch.batch``, ``batch.ptr``, ``batch.num_graphs``,
     ``batch.to(device)``), plus the batch CSR."""
 
-    def __init__(self, store: dict, num_graphs: int, csr=None):
+    def __init__(self, store: dict, num_graphs: int, csr=None, graph: SageGraph | None = None):
         object.__setattr__(self, "_store", store)
         object.__setattr__(self, "num_graphs", num_graphs)
-        object.__setattr__(self, "_csr", csr)   # (N, E, rowptr, col, t_rowptr, t_col)
+        object.__setattr__(self, "_csr", csr)   # host (N, E, rowptr, col, t_rowptr, t_col)
+        object.__setattr__(self, "_graph", graph)   # device SageGraph (GPU batching path)
 
     def __getattr__(self, key):
         try:
@@ -147,18 +148,25 @@ class GraphBatch:
     def sage_graph(self, device=None) -> SageGraph | None:
         """The batch CSR as a :class:`SageGraph` on ``device`` (default: where
         ``edge_index`` lives)."""
+        dev = torch.device(device) if device is not None else self._store["edge_index"].device
+        if self._graph is not None and self._graph.device == dev:
+            return self._graph
         if self._csr is None:
             return None
         n, e, rp, col, trp, tcol = self._csr
-        dev = torch.device(device) if device is not None else self._store["edge_index"].device
         t = [torch.as_tensor(a).to(dev) for a in (rp, col, trp, tcol)]
         return SageGraph(n, e, t[0], t[1], t[2], t[3])
 
     def to(self, device, non_blocking: bool = False) -> "GraphBatch":
         store = {k: (v.to(device, non_blocking=non_blocking) if isinstance(v, torch.Tensor) else v)
                  for k, v in self._store.items()}
-        out = GraphBatch(store, self.num_graphs, self._csr)
         ei = store.get("edge_index")
+        g = self._graph if (self._graph is not None and isinstance(ei, torch.Tensor)
+                            and ei.device == self._graph.device) else None
+        out = GraphBatch(store, self.num_graphs, self._csr, g)
+        if g is not None:
+            graph_cache.put(ei, g.num_nodes, g)
+            return out
         if self._csr is not None and isinstance(ei, torch.Tensor) and ei.device.type == "cuda":
             graph_cache.put(ei, self._csr[0], out.sage_graph(ei.device))
         return out
@@ -167,6 +175,29 @@ class GraphBatch:
         parts = [f"{k}={list(v.shape) if isinstance(v, torch.Tensor) else type(v).__name__}"
                  for k, v in self._store.items()]
         return f"GraphBatch(num_graphs={self.num_graphs}, {', '.join(parts)})"
+
+
+def _device_batch(items, counts):
+    """The fused GPU batching path (ops.batch_graphs) when every graph's
+    edge_index is an int64 [2, E] tensor on one GPU and no graph exceeds the
+    kernel's node limit; None otherwise (host path below)."""
+    eis = [d.get("edge_index") for d in items]
+    if not eis or not all(isinstance(e, torch.Tensor) for e in eis):
+        return None
+    dev = eis[0].device
+    if dev.type != "cuda" or any(
+            e.device != dev or e.dtype != torch.int64 or e.dim() != 2 or e.size(0) != 2
+            or (e.size(1) > 1 and e.stride(1) != 1) for e in eis):
+        return None
+    from . import _lib, ops
+    if max(counts) > _lib.load().sldm_batch_graphs_max_nodes():
+        return None
+    ei, batch, ptr, rowptr, col, t_rowptr, t_col, bad = ops.batch_graphs(eis, counts)
+    if int(bad.item()):                       # the batch's one host sync
+        raise IndexError("edge_index holds a node id outside its graph's [0, num_nodes) "
+                         "(the reference's index_select/scatter would raise as well)")
+    graph = SageGraph(int(sum(counts)), int(ei.size(1)), rowptr, col, t_rowptr, t_col)
+    return ei, batch, ptr, graph
 
 
 def collate(data_list) -> GraphBatch:
@@ -179,6 +210,12 @@ def collate(data_list) -> GraphBatch:
     offs = np.zeros(len(items) + 1, np.int64)
     np.cumsum(counts, out=offs[1:])
     store: dict = {}
+    fused = _device_batch(items, counts)
+    if fused is not None:
+        # graphs on the GPU: edge_index + batch + ptr + the batch CSR pair in
+        # one kernel (ops.batch_graphs), registered for the SageBlock
+        store["edge_index"], store["batch"], store["ptr"] = fused[:3]
+        keys = [k for k in keys if k != "edge_index"]
     for k in keys:
         vals = [d[k] for d in items]
         v0 = vals[0]
@@ -195,17 +232,20 @@ def collate(data_list) -> GraphBatch:
         else:
             store[k] = vals
     N = int(offs[-1])
+    if fused is not None:
+        graph_cache.put(store["edge_index"], N, fused[3])
+        return GraphBatch(store, len(items), None, fused[3])
     dev = next((v.device for v in store.values() if isinstance(v, torch.Tensor)),
                torch.device("cpu"))
     store["batch"] = torch.repeat_interleave(
-        torch.arange(len(items), device=dev), torch.tensor(counts, device=dev))
+        torch.arange(len(items), device=dev), torch.tensor(counts, device=dev),
+        output_size=N)
     store["ptr"] = torch.as_tensor(offs, device=dev)
     csr = None
     # The batch CSR is assembled on the host from per-graph host CSRs when the
-    # graphs live on the host (the DataLoader-worker case).  Graphs already on
-    # the GPU (dataset.py:77 loads with map_location=DEVICE) keep theirs off:
-    # reading every graph's edge_index back would cost one device sync per
-    # graph, where the SageBlock builds the batch CSR on the GPU with one.
+    # graphs live on the host (the DataLoader-worker case).  Graphs on the GPU
+    # (dataset.py:77 loads with map_location=DEVICE) took the fused path above;
+    # the rest (e.g. int32 ids) leave the CSR to the SageBlock's GPU build.
     if "edge_index" in items[0] and all(
             getattr(d.get("edge_index"), "device", torch.device("cpu")).type == "cpu"
             for d in items):

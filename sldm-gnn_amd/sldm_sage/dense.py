@@ -29,12 +29,15 @@ def sage_layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p, seed, sa
 
 
 def sage_linear_bwd_data(dh: torch.Tensor, wl: torch.Tensor, wr: torch.Tensor,
-                         rowptr: torch.Tensor):
+                         rowptr: torch.Tensor, wcat: torch.Tensor | None = None):
     """[dAgg / deg | dx_root] = dh · [W_l | W_r] in one launch; returns the
     prescaled aggregate grad and the root-path grad as two contiguous [N, F_in]
-    tensors (F_in % 4 == 0; otherwise column views of one [N, 2 F_in] buffer)."""
+    tensors (F_in % 4 == 0; otherwise column views of one [N, 2 F_in] buffer).
+    ``wcat``: the forward's [W_l | W_r] operand (saves rebuilding it)."""
     fi = wl.size(1)
-    wcat_t = weight_cat(wl, wr, dh.dtype).t().contiguous()     # [2 F_in, F_out]
+    if wcat is None or wcat.dtype != dh.dtype:
+        wcat = weight_cat(wl, wr, dh.dtype)
+    wcat_t = wcat.t().contiguous()                              # [2 F_in, F_out]
     if fi % 4 == 0:
         return ops.gemm_nt_rowscale(dh, wcat_t, rowptr, scale_cols=fi, split=True)
     buf = ops.gemm_nt_rowscale(dh, wcat_t, rowptr, scale_cols=fi)

@@ -109,6 +109,47 @@ def csr_build(edge_index: torch.Tensor, num_nodes: int, transpose: bool = True):
     return rowptr, col, t_rowptr, t_col, bad
 
 
+def batch_graphs(edge_indices, num_nodes, transpose: bool = True):
+    """PyG Batch.from_data_list for G device-resident edge_index tensors, fused
+    with the batch CSR pair (``sldm_batch_graphs``, batch.hip).
+
+    edge_indices: int64 [2, E_g] on one GPU (unit column stride); num_nodes:
+    N_g per graph.  Returns (edge_index [2, E], batch [N], ptr [G+1], rowptr,
+    col, t_rowptr, t_col, bad) -- ``bad`` as in :func:`csr_build`.
+    """
+    import ctypes
+    dev = _require_gpu(*edge_indices)
+    G = len(edge_indices)
+    for ei in edge_indices:
+        if ei.dtype != torch.int64 or ei.dim() != 2 or ei.size(0) != 2 or (
+                ei.size(1) > 1 and ei.stride(1) != 1) or ei.device != dev:
+            raise ValueError("batch_graphs: edge_index must be int64 [2, E] with unit column "
+                             "stride on one device")
+    ne = [int(ei.size(1)) for ei in edge_indices]
+    nn = [int(n) for n in num_nodes]
+    E, N = sum(ne), sum(nn)
+    lib = _lib.load()
+    out_ei = torch.empty(2, E, dtype=torch.int64, device=dev)
+    bp = torch.empty(N + G + 1, dtype=torch.int64, device=dev)
+    nt = 2 if transpose else 1
+    buf = torch.empty(nt * (N + 1 + E) + 1, dtype=torch.int32, device=dev)
+    rowptr, col = buf[:N + 1], buf[N + 1:N + 1 + E]
+    t_rowptr = buf[N + 1 + E:2 * (N + 1) + E] if transpose else None
+    t_col = buf[2 * (N + 1) + E:2 * (N + 1 + E)] if transpose else None
+    bad = buf[-1:]
+    ptrs = (ctypes.c_void_p * G)(*[ei.data_ptr() for ei in edge_indices])
+    strides = (ctypes.c_int64 * G)(*[ei.stride(0) if ei.size(1) else 0 for ei in edge_indices])
+    c_ne = (ctypes.c_int64 * G)(*ne)
+    c_nn = (ctypes.c_int64 * G)(*nn)
+    with _Timed("batch_graphs", E):
+        _lib.check(lib.sldm_batch_graphs(G, ptrs, strides, c_ne, c_nn, out_ei.data_ptr(), E,
+                                         bp.data_ptr(), bp[N:].data_ptr(), rowptr.data_ptr(),
+                                         col.data_ptr(), _ptr(t_rowptr), _ptr(t_col),
+                                         bad.data_ptr(), _stream(dev)),
+                   "sldm_batch_graphs")
+    return out_ei, bp[:N], bp[N:], rowptr, col, t_rowptr, t_col, bad
+
+
 def degree_order(rowptr: torch.Tensor) -> torch.Tensor:
     """Rows by decreasing degree (stable): the longest-first gather schedule."""
     dev = _require_gpu(rowptr)

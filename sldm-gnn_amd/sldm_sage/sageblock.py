@@ -81,9 +81,11 @@ class _SageLayerFn(torch.autograd.Function):
         agg = ops.gather_rows(x, graph.rowptr, graph.col, n, mean=True, name="gather_fwd",
                               order=graph.order, hub=graph.hub)
         needs_grad = any(ctx.needs_input_grad[:6])
+        wcat = dense.weight_cat(wl, wr, x.dtype)
         out, xhat, rstd = dense.sage_layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope,
-                                               drop_p, seed, save=needs_grad)
+                                               drop_p, seed, save=needs_grad, wcat=wcat)
         if needs_grad:
+            ctx.wcat = wcat
             # `out` is saved too (it is the next layer's input anyway): with
             # SLDM_ACT_BRANCH_FROM_OUTPUT=1 its sign picks the activation
             # branch in the backward (ops.branch_source).
@@ -107,7 +109,7 @@ class _SageLayerFn(torch.autograd.Function):
                                    "transpose=True for backward")
             # [dAgg/deg | dx_root] in one MFMA pass, then the transpose gather
             # adds the root-path gradient as it sums over out-edges.
-            g, dx_r = dense.sage_linear_bwd_data(dh, wl, wr, graph.rowptr)
+            g, dx_r = dense.sage_linear_bwd_data(dh, wl, wr, graph.rowptr, wcat=ctx.wcat)
             dx = ops.gather_rows(g, graph.t_rowptr, graph.t_col, x.size(0), mean=False,
                                  order=graph.t_order, hub=graph.t_hub,
                                  addend=dx_r, name="gather_bwd")
@@ -148,17 +150,20 @@ class _SageStackFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, graph: SageGraph, cfgs, *params):
         n = x.size(0)
-        saved = []
+        saved, wcats = [], []
         h = x
         for i, (slope, drop_p, seed, eps) in enumerate(cfgs):
             wl, bl, wr, gamma, beta = params[5 * i: 5 * i + 5]
             agg = ops.gather_rows(h, graph.rowptr, graph.col, n, mean=True, name="gather_fwd",
                                   order=graph.order, hub=graph.hub)
+            wcat = dense.weight_cat(wl, wr, h.dtype)
             out, xhat, rstd = dense.sage_layer_fwd(agg, h, wl, bl, wr, gamma, beta, eps, slope,
-                                                   drop_p, seed, save=True)
+                                                   drop_p, seed, save=True, wcat=wcat)
             saved += [h, agg, xhat, rstd]
+            wcats.append(wcat)
             h = out
         ctx.save_for_backward(*saved, *params)
+        ctx.wcats = wcats
         ctx.graph, ctx.cfgs, ctx.nl = graph, cfgs, len(cfgs)
         return h
 
@@ -202,7 +207,7 @@ class _SageStackFn(torch.autograd.Function):
                                        dbeta.to(beta.dtype)]
             if i == 0 and not ctx.needs_input_grad[0]:
                 break
-            g, dx_r = dense.sage_linear_bwd_data(dh, wl, wr, graph.rowptr)
+            g, dx_r = dense.sage_linear_bwd_data(dh, wl, wr, graph.rowptr, wcat=ctx.wcats[i])
             if i == 0:
                 dx = ops.gather_rows(g, graph.t_rowptr, graph.t_col, h.size(0), mean=False,
                                      order=graph.t_order, hub=graph.t_hub, addend=dx_r, name="gather_bwd")

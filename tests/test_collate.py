@@ -113,3 +113,82 @@ def test_collate_csr_registered_on_device_and_used():
     graph_cache.clear()
     out_b = blk(x, b.edge_index)                    # GPU-built CSR
     assert torch.equal(out_a, out_b)
+
+
+def _device_graphs(spec, seed=0):
+    """Graphs on the GPU with awkward edge lists: duplicates, self loops,
+    unsorted ids, a star (one row of high degree), an edge_index that is a
+    column slice of a wider buffer (row stride > E), empty graphs."""
+    out = []
+    g = torch.Generator().manual_seed(seed)
+    for i, (n, e, kind) in enumerate(spec):
+        if kind == "star":
+            src = torch.randint(0, n, (e,), generator=g)
+            ei = torch.stack([src, torch.zeros(e, dtype=torch.long)])
+        else:
+            ei = torch.randint(0, max(n, 1), (2, e), generator=g) if n else \
+                torch.empty(2, 0, dtype=torch.long)
+        ei = ei.cuda()
+        if kind == "strided":
+            wide = torch.full((2, e + 7), -5, dtype=torch.long, device="cuda")
+            wide[:, :e] = ei
+            ei = wide[:, :e]
+        out.append({"x": torch.randn(n, 8, generator=g).cuda(), "edge_index": ei})
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", [
+    [(250, 6000, ""), (300, 9000, ""), (0, 0, ""), (1, 3, ""), (40, 0, ""), (220, 5000, "strided")],
+    [(n, 8 * n, "") for n in range(1, 60)],                 # > 48 graphs: two launches
+    [(2000, 3000, "star"), (5, 40, ""), (16384, 20000, "")],  # high degree, max nodes
+])
+def test_device_collate_fused_batch_matches_pyg_and_csr_build(spec):
+    """The fused GPU batching kernel (batch.hip): edge_index / batch / ptr as
+    Batch.from_data_list, and the batch CSR pair bit-equal to sldm_csr_build on
+    the batched edge_index (row order = original edge order)."""
+    from sldm_sage import graph_cache, ops
+    from sldm_sage.data import collate
+    graphs = _device_graphs(spec)
+    b = collate(graphs)
+    counts = [d["x"].size(0) for d in graphs]
+    offs = [0]
+    for c in counts:
+        offs.append(offs[-1] + c)
+    want_ei = torch.cat([d["edge_index"] + offs[i] for i, d in enumerate(graphs)], 1)
+    assert torch.equal(b.edge_index, want_ei)
+    assert torch.equal(b.ptr.cpu(), torch.tensor(offs))
+    assert torch.equal(b.batch.cpu(), torch.repeat_interleave(torch.arange(len(graphs)),
+                                                              torch.tensor(counts)))
+    assert torch.equal(b.x, torch.cat([d["x"] for d in graphs]))
+    g = b.sage_graph()
+    assert g is not None and graph_cache.get(b.edge_index, b.num_nodes, True) is g
+    rp, col, trp, tcol, _ = ops.csr_build(b.edge_index, b.num_nodes, True)
+    for got, exp in zip((g.rowptr, g.col, g.t_rowptr, g.t_col), (rp, col, trp, tcol)):
+        assert torch.equal(got, exp)
+
+
+@pytest.mark.gpu
+def test_device_collate_bad_id_raises_and_sageblock_uses_fused_csr():
+    from sldm_sage import SageBlock, graph_cache
+    from sldm_sage.data import collate
+    graphs = _device_graphs([(30, 100, ""), (20, 50, "")], seed=3)
+    bad = [dict(graphs[0]), dict(graphs[1])]
+    bad[1]["edge_index"] = bad[1]["edge_index"].clone()
+    bad[1]["edge_index"][1, 7] = 20                  # == N_g: outside its own graph
+    with pytest.raises(IndexError):
+        collate(bad)
+    b = collate(graphs)
+    torch.manual_seed(0)
+    blk = SageBlock([8, 16, 16], 0.25, 0.1).cuda().train()
+    x = b.x.detach().requires_grad_(True)
+    torch.manual_seed(5)
+    out_a = blk(x, b.edge_index)
+    out_a.sum().backward()
+    ga = x.grad.clone()
+    graph_cache.clear()                              # rebuild with sldm_csr_build
+    x.grad = None
+    torch.manual_seed(5)
+    out_b = blk(x, b.edge_index)
+    out_b.sum().backward()
+    assert torch.equal(out_a, out_b) and torch.equal(ga, x.grad)

@@ -32,7 +32,7 @@ pool = [bench._synthetic_pack(gen, dev, 250, 128) for _ in range(32)]
 torch.manual_seed(0)
 blk = SageBlock([128, 96, 96], 0.25, 0.1).to(dev).train()
 b = collate([dict(p) for p in pool])
-h, ei = b.h, b.edge_index
+h, ei = b.x, b.edge_index
 print("nodes", h.size(0), "edges", ei.size(1))
 print("collate ms", tm(lambda: collate([dict(p) for p in pool])))
 print("csr build ms", tm(lambda: build_graph(ei, h.size(0))))
