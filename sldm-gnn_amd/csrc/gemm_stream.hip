@@ -48,6 +48,11 @@ constexpr int NSTW = 4;           // weight ring stages
 #define SLDM_STREAM_DA 4
 #endif
 constexpr int DA = SLDM_STREAM_DA;
+// Diagnostic builds only (tools/ab_build.sh): 1 = the LN kernel storing z
+// without LayerNorm / activation / dropout (results wrong).
+#ifndef SLDM_STREAM_EXP
+#define SLDM_STREAM_EXP 0
+#endif
 constexpr int SROW = 512 + 16;    // LN staging row stride in bytes (conflict-free b64 writes)
 
 enum { ST_LN = 0, ST_ROWSCALE = 1 };
@@ -296,6 +301,11 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
         // included) makes their stores identical rewrites of row M-1.
         const int64_t row0 = tile * BM + wr * RW + 16 * m;   // first row of this 16-row slab
         const int64_t row = min(row0 + r16, p.M - 1);
+#if SLDM_STREAM_EXP == 1
+        const float rs = 1.f;   // diagnostic build: no LayerNorm / activation / dropout
+        const uint32_t rkey = 0;
+        (void)rkey;
+#else
         // acc <- acc + bias; mean; acc <- (acc - mean); var; acc <- acc * rstd = xhat
         float s = 0.f;
 #pragma unroll
@@ -322,8 +332,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
         const float rs = 1.0f / sqrtf(v2 * inv_n + p.eps);
 #pragma unroll
         for (int t = 0; t < NTT; ++t) acc[m][t] *= rs;
-        if (p.rstd && q == 0) p.rstd[row] = rs;
         const uint32_t rkey = sldm::dropout_row_key(p.seed, (uint64_t)(row + p.row_off));
+#endif
+        if (p.rstd && q == 0) p.rstd[row] = rs;
 
         // two staging rounds through the wave's 16 x 512 B tile: xhat, then out
 #pragma unroll
@@ -334,7 +345,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
           for (int t = 0; t < NTT; ++t) {
             const int c = 16 * t + cq;
             float v[4];
-            if (pass == 0) {
+            if (pass == 0 || SLDM_STREAM_EXP == 1) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] = acc[m][t][r];
             } else {

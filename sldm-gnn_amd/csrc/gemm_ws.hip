@@ -257,6 +257,11 @@ struct WsLnArgs {
 #define SLDM_WSLN_PF 2
 #endif
 constexpr int WSLN_PF = SLDM_WSLN_PF;
+// Diagnostic builds only (tools/ab_build.sh): 1 = the exchange kernel with a
+// plain store epilogue, 2 = without its MFMAs.  Results are wrong in both.
+#ifndef SLDM_WSLN_EXP
+#define SLDM_WSLN_EXP 0
+#endif
 
 template <int KSTEPS, int NBUF, int TM, bool XCHG>
 constexpr size_t ws_ln_lds_bytes() {
@@ -409,12 +414,40 @@ __global__ __launch_bounds__(kThreads) void ws_ln_kernel(WsLnArgs p) {
       for (int m = 0; m < RG; ++m)
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
+#if SLDM_WSLN_EXP == 2
+          acc[m][ct] += __builtin_bit_cast(f4v, __builtin_shufflevector(bf[s % (PF + 1)][m],
+                                                                        bf[s % (PF + 1)][m], 0, 1, 2, 3, 4, 5, 6, 7));
+#else
           acc[m][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ct][s], bf[s % (PF + 1)][m],
                                                               acc[m][ct], 0, 0, 0);
+#endif
       if (s + PF < KSTEPS) __builtin_amdgcn_sched_group_barrier(0x100, RG, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, RG * CT, 0);
     }
 
+#if SLDM_WSLN_EXP == 1
+    if constexpr (XCHG) {   // experiment: main loop + plain bf16 stores of z
+      const int64_t r0 = tile * TM;
+      const int ccol = cbase + ((q & 1) ? 16 + 4 * (q - 1) : 4 * q);
+#pragma unroll
+      for (int m = 0; m < RG; ++m) {
+        const int64_t row = r0 + 16 * m + i < p.M ? r0 + 16 * m + i : p.M - 1;
+        uint32_t w[2][2];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          w[ct][0] = sldm::pack_bf16x2(acc[m][ct][0], acc[m][ct][1]);
+          w[ct][1] = sldm::pack_bf16x2(acc[m][ct][2], acc[m][ct][3]);
+        }
+        auto s0 = __builtin_amdgcn_permlane16_swap(w[0][0], w[1][0], false, false);
+        auto s1 = __builtin_amdgcn_permlane16_swap(w[0][1], w[1][1], false, false);
+        const uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        if (hasx) *reinterpret_cast<uint4*>(p.xhat + row * 256 + ccol) = v;
+        *reinterpret_cast<uint4*>(p.out + row * 256 + ccol) = v;
+      }
+      if (p.rstd && lane < 32) p.rstd[r0 + lane < p.M ? r0 + lane : p.M - 1] = 1.f;
+      continue;
+    }
+#endif
     if constexpr (XCHG) {
       // ---- epilogue, exchange form: acc[m][ct][r] = z[row 16m + i][col
       // cbase + 16ct + 4q + r] stays in place.  Row sums: in-lane over the
@@ -424,7 +457,8 @@ __global__ __launch_bounds__(kThreads) void ws_ln_kernel(WsLnArgs p) {
       // buffers, so tile n+1's first exchange never races tile n's reads (every
       // wave has read buffer 0 before it reaches the second barrier).
       float* red = reinterpret_cast<float*>(zs);
-      auto row_total = [&](float (&part)[RG], int buf, float (&tot)[RG]) {
+      float tot[RG];
+      auto row_total = [&](float (&part)[RG], int buf, float (&sum)[RG]) {
 #pragma unroll
         for (int m = 0; m < RG; ++m) {
           float v = part[m];
@@ -437,10 +471,10 @@ __global__ __launch_bounds__(kThreads) void ws_ln_kernel(WsLnArgs p) {
         for (int m = 0; m < RG; ++m) {
           const f4v* pr = reinterpret_cast<const f4v*>(red + (buf * TM + 16 * m + i) * 8);
           const f4v a = pr[0], b = pr[1];
-          tot[m] = a[0] + a[1] + a[2] + a[3] + b[0] + b[1] + b[2] + b[3];
+          sum[m] = a[0] + a[1] + a[2] + a[3] + b[0] + b[1] + b[2] + b[3];
         }
       };
-      float part[RG], tot[RG];
+      float part[RG];
 #pragma unroll
       for (int m = 0; m < RG; ++m) {
         part[m] = 0.f;
