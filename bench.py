@@ -494,6 +494,13 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize(dev)
 
+    link_bps = None
+    if use_dist:
+        # the node's achieved xGMI rate, measured once, prices the planner's
+        # exchanges (RCCL only; gloo rehearsals keep the model constant)
+        from sldm_sage.dist import measure_link_bps
+        link_bps = measure_link_bps(dev)
+
     def run(kind, timed_kernels):
         """Build the workload on graph ``kind``, warm up, time args.steps steps
         (max over ranks).  Returns (elapsed_s, kernel summary, dist info, incl)."""
@@ -506,7 +513,7 @@ def main():
         if use_dist:
             from sldm_sage.dist import DistSageBlock, plan_partition
             part, plan = plan_partition(ei, n, world, rank, f, x.element_size(),
-                                        strategy=args.strategy)
+                                        strategy=args.strategy, link_bps=link_bps)
             model = DistSageBlock(blk, part)
             x_in = x[part.row_begin:part.row_end].contiguous()
             g_in = gout[part.row_begin:part.row_end].contiguous()
@@ -515,7 +522,10 @@ def main():
                              part.exchange_bytes_per_layer(f, x.element_size())}
             if "halo_s" not in plan:       # forced strategy: still price every option
                 from sldm_sage.dist import estimate_strategies
-                plan.update(estimate_strategies(ei, n, world, rank, f, x.element_size()))
+                plan.update(estimate_strategies(ei, n, world, rank, f, x.element_size(),
+                                                link_bps=link_bps))
+            dist_info["link_bps_measured"] = link_bps
+            dist_info["link_bps_model"] = plan.get("link_bps")
             for k in ("halo_s", "feature_s", "replicate_s"):
                 dist_info[f"model_{k[:-2]}_ms_per_layer"] = round(plan[k] * 1e3, 3)
             # the planner's prediction for this run (sldm_sage.dist cost model,

@@ -58,6 +58,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import time
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -891,12 +893,39 @@ def choose_strategy(info: dict) -> str:
     return best if info[f"{best}_s"] * _PARTITION_MARGIN < info["replicate_s"] else "replicate"
 
 
+def measure_link_bps(device: torch.device, group=None, per_peer_bytes: int = 32 << 20,
+                     reps: int = 3) -> float | None:
+    """Achieved per-peer rate (bytes/s, one direction) of a balanced
+    all_to_all over RCCL on this node: every rank sends ``per_peer_bytes`` to
+    every peer at once (the feature-slicing switch pattern), timed after one
+    warm-up call, max over ranks.  None when the group is not NCCL / RCCL or
+    has one rank (the planner then keeps ``_LINK_BPS``)."""
+    world = dist.get_world_size(group)
+    if world < 2 or dist.get_backend(group) != "nccl" or device.type != "cuda":
+        return None
+    n = per_peer_bytes // 2
+    inp = torch.empty(world * n, dtype=torch.bfloat16, device=device).normal_()
+    out = torch.empty_like(inp)
+    dist.all_to_all_single(out, inp, group=group)          # warm-up (connections)
+    torch.cuda.synchronize(device)
+    dist.barrier(group=group)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.all_to_all_single(out, inp, group=group)
+    torch.cuda.synchronize(device)
+    t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return per_peer_bytes / float(t)
+
+
 def estimate_strategies(edge_index: torch.Tensor, num_nodes: int, world: int, rank: int,
-                        feat: int, elem: int, group=None) -> dict:
+                        feat: int, elem: int, group=None, link_bps: float | None = None) -> dict:
     """Modelled per-layer time (s) of the halo, feature-sliced and replicated
     strategies: exchange bytes / xGMI + gather bytes / measured gather rate +
     dense bytes / stream rate, max over ranks (collective over ``group`` when
-    world > 1, so every rank gets the same numbers)."""
+    world > 1, so every rank gets the same numbers).  ``link_bps``: the
+    per-peer xGMI rate to price exchanges at (:func:`measure_link_bps`;
+    default ``_LINK_BPS``)."""
     hb_ = row_bounds(edge_index, num_nodes, world, "cost")     # partition_graph's blocks
     h0, h1 = hb_[rank], hb_[rank + 1]
     src, dst = edge_index[0], edge_index[1]
@@ -905,7 +934,7 @@ def estimate_strategies(edge_index: torch.Tensor, num_nodes: int, world: int, ra
     halo_f = _remote_unique(src[in_mask], h0, h1)
     halo_b = _remote_unique(dst[out_mask], h0, h1)
     e_in, e_out = int(in_mask.sum()), int(out_mask.sum())
-    link = max(world - 1, 1) * _LINK_BPS
+    link = max(world - 1, 1) * (link_bps or _LINK_BPS)
     row = feat * elem
     halo_t = ((halo_f + halo_b) * row / link
               + (e_in + e_out) * (row + 4) / _gather_rate(row)
@@ -930,7 +959,8 @@ def estimate_strategies(edge_index: torch.Tensor, num_nodes: int, world: int, ra
         all_reduce(v, op=dist.ReduceOp.MAX, group=group)
     halo_t, feat_t, rep_t, hf, hb = v.tolist()
     return {"halo_s": halo_t, "feature_s": feat_t, "replicate_s": rep_t,
-            "halo_rows_fwd_max": int(hf), "halo_rows_bwd_max": int(hb)}
+            "halo_rows_fwd_max": int(hf), "halo_rows_bwd_max": int(hb),
+            "link_bps": float(link_bps or _LINK_BPS)}
 
 
 @dataclass
@@ -971,7 +1001,8 @@ def partition_replicated(edge_index: torch.Tensor, num_nodes: int, world: int, r
 
 def plan_partition(edge_index: torch.Tensor, num_nodes: int, world: int, rank: int,
                    feat: int, elem: int, strategy: str = "auto", backend=HipBackend,
-                   group=None, chunks: int = 4, balance: str = "cost"):
+                   group=None, chunks: int = 4, balance: str = "cost",
+                   link_bps: float | None = None):
     """Partition with ``strategy`` in {"auto", "halo", "feature", "replicate"};
     "auto" takes :func:`choose_strategy` of :func:`estimate_strategies`
     (every rank gets the same answer: the estimate is max-reduced).  Returns
@@ -982,7 +1013,8 @@ def plan_partition(edge_index: torch.Tensor, num_nodes: int, world: int, rank: i
         if world == 1:
             strategy = "halo"
         else:
-            info = estimate_strategies(edge_index, num_nodes, world, rank, feat, elem, group)
+            info = estimate_strategies(edge_index, num_nodes, world, rank, feat, elem, group,
+                                       link_bps)
             strategy = choose_strategy(info)
     info["strategy"] = strategy
     if strategy == "feature":
