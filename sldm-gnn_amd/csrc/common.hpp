@@ -143,6 +143,14 @@ __device__ __forceinline__ void store_vec(T* p, const float* r) {
 // Mode bits: 1 = output stores, 2 = source-row loads.  SLDM_GATHER_NT in the
 // environment forces a mode: 0 none, s stores only, 1 both (read per call).
 constexpr int64_t kNtTableBytes = (int64_t)1 << 30;
+// Per-row streamed operands of the gathers (the addend row, the LN backward's
+// xhat row): loaded non-temporal too in the non-temporal (GiB-table) mode.
+// Same-box A/B at C4 (kbench): fused layer boundary 12.10 -> 11.52 ms,
+// transpose gather + addend 10.49 -> 10.34 ms, forward gather unchanged.
+#ifndef SLDM_STREAM_OPERANDS_NT
+#define SLDM_STREAM_OPERANDS_NT 1
+#endif
+constexpr bool kStreamOperandsNt = SLDM_STREAM_OPERANDS_NT != 0;
 inline int nt_gather(int64_t table_bytes) {
   const char* e = getenv("SLDM_GATHER_NT");
   if (e && e[0] == '0') return 0;

@@ -97,7 +97,9 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(
   if constexpr (ADD) {
     if (!chunk) {
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) sldm::Vec<TO, V>::load(addend + row * lda + f0[c], a[c]);
+      for (int c = 0; c < NCH; ++c)
+        sldm::load_vec<TO, V, sldm::kStreamOperandsNt && (NT & 1) != 0>(addend + row * lda + f0[c],
+                                                                         a[c]);
     }
   }
 

@@ -110,8 +110,10 @@ __global__ __launch_bounds__(kBlock) void gather_post_bwd_kernel(
     float xh[NCH][V], ad[NCH][V];
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      sldm::Vec<T, V>::load(xhat + row * (int64_t)feat + f0[c], xh[c]);
-      sldm::Vec<T, V>::load(addend + row * lda + f0[c], ad[c]);
+      sldm::load_vec<T, V, sldm::kStreamOperandsNt && (NT & 1) != 0>(
+          xhat + row * (int64_t)feat + f0[c], xh[c]);
+      sldm::load_vec<T, V, sldm::kStreamOperandsNt && (NT & 1) != 0>(addend + row * lda + f0[c],
+                                                                      ad[c]);
     }
     const float rs = rstd[row];
 
