@@ -248,6 +248,19 @@ __device__ __forceinline__ float group_sum(float v, int g) {
   return v;
 }
 
+// Sum over the four 16-lane rows of a wave (lanes l, l^16, l^32, l^48: an MFMA
+// C-layout row's four column groups), result bitwise identical in all four:
+// two gfx950 VALU lane swaps (v_permlane16_swap, v_permlane32_swap) instead of
+// ds_swizzle + ds_bpermute round trips through the LDS crossbar.
+__device__ __forceinline__ float row4_sum(float v) {
+  const uint32_t u = __float_as_uint(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  const float v2 = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const uint32_t u2 = __float_as_uint(v2);
+  const auto b = __builtin_amdgcn_permlane32_swap(u2, u2, false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 // Big-tile bf16 dense kernels (gemm_big.hip); the gemm.hip entry points route
 // conforming shapes to them.  SLDM_BIG_GEMM=0 in the environment disables them
 // (A/B comparisons against the 64-row kernels).

@@ -315,8 +315,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
 #pragma unroll
           for (int r = 0; r < 4; ++r) s += acc[m][t][r];
         }
-        s += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(s), 0x401F));
-        s += __shfl_xor(s, 32, 64);
+        s = sldm::row4_sum(s);
         const float mean = s * inv_n;
         float v2 = 0.f;
 #pragma unroll
@@ -327,8 +326,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
             acc[m][t][r] = d;
             v2 += d * d;
           }
-        v2 += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v2), 0x401F));
-        v2 += __shfl_xor(v2, 32, 64);
+        v2 = sldm::row4_sum(v2);
         const float rs = 1.0f / sqrtf(v2 * inv_n + p.eps);
 #pragma unroll
         for (int t = 0; t < NTT; ++t) acc[m][t] *= rs;

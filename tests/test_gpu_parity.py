@@ -658,12 +658,13 @@ STREAM_ROWS = [1, 255, 256, 257, 2000, 70_001]
 
 @pytest.mark.parametrize("m", STREAM_ROWS + [63, 65])
 @pytest.mark.parametrize("fi", [128, 256])
-@pytest.mark.parametrize("kernel", ["ws", "ws_xchg", "stream"])
+@pytest.mark.parametrize("kernel", ["ws", "ws_xchg", "ws_pipe", "stream"])
 def test_stream_dense_fwd_vs_torch_and_mask(m, fi, kernel, monkeypatch):
     """The bf16 forward kernels: gemm_ws.hip (weights in VGPRs; z re-distributed
     through LDS, or only the LayerNorm partial sums exchanged across the 8
     waves) and gemm_stream.hip."""
-    monkeypatch.setenv("SLDM_WS_FWD", {"ws": "1", "ws_xchg": "2", "stream": "0"}[kernel])
+    monkeypatch.setenv("SLDM_WS_FWD", {"ws": "1", "ws_xchg": "2", "ws_pipe": "3",
+                                       "stream": "0"}[kernel])
     from sldm_sage import ops
     from sldm_sage.dense import weight_cat
     fo, p, seed = 256, 0.25, 4242
@@ -719,7 +720,7 @@ def test_tn_dma_weight_grad_vs_torch(rows, n1, monkeypatch):
 
 @pytest.mark.parametrize("m", [1, 65, 4097, 130_000])
 @pytest.mark.parametrize("k0,k1", [(256, 256), (128, 128), (256, 0), (512, 0), (128, 384)])
-@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("mode", ["1", "2", "3"])
 def test_ws_dense_fwd_matches_stream(m, k0, k1, mode, monkeypatch):
     """The weight-stationary forwards (SLDM_WS_FWD=1: z re-distributed through
     LDS; 2: LayerNorm partial sums exchanged) and the stream kernel differ only
@@ -751,6 +752,15 @@ def test_ws_dense_fwd_matches_stream(m, k0, k1, mode, monkeypatch):
     torch.testing.assert_close(r1, r2, atol=0, rtol=1e-5)
     torch.testing.assert_close(x1.float(), x2.float(), atol=1e-2, rtol=1e-2)
     torch.testing.assert_close(o1.float(), o2.float(), atol=3e-2, rtol=1e-2)
+    # inference form (no xhat / rstd saved): the same outputs
+    monkeypatch.setenv("SLDM_WS_FWD", mode)
+    o3 = torch.full((m, 256), 7.0, dtype=torch.bfloat16, device=DEV)
+    ops._lib.check(ops._lib.load().sldm_sage_dense_fwd(
+        ops.dtype_code(a0), a0.data_ptr(), a0.stride(0), k0, a1.data_ptr(), a1.stride(0), k1,
+        w.data_ptr(), m, 256, b.data_ptr(), g.data_ptr(), be.data_ptr(), 1e-5, 0.1, 0.3, 99, 0,
+        o3.data_ptr(), None, None, ops._stream(torch.device(DEV))), "sldm_sage_dense_fwd")
+    torch.cuda.synchronize()
+    assert torch.equal(o3, o1)
 
 
 @pytest.mark.parametrize("m", STREAM_ROWS)

@@ -81,7 +81,9 @@ def main():
                 fl)
         for var, env, p_ in [("ws", {"SLDM_WS_FWD": "1"}, 0.25),
                              ("ws_xchg", {"SLDM_WS_FWD": "2"}, 0.25),
-                             ("ws_xchg", {"SLDM_WS_FWD": "2"}, 0.0)]:
+                             ("ws_xchg", {"SLDM_WS_FWD": "2"}, 0.0),
+                             ("ws_pipe", {"SLDM_WS_FWD": "3"}, 0.25),
+                             ("ws_pipe", {"SLDM_WS_FWD": "3"}, 0.0)]:
             os.environ.update(env)
             ms = timeit(lambda: ops.sage_dense_fwd(agg, x, wcat, b, gam, bet, 1e-5, 0.1, p_, 7,
                                                    True), a.reps)
