@@ -40,6 +40,7 @@ g = build_graph(ei, h.size(0))
 
 
 def ours():
+    blk.zero_grad(set_to_none=True)
     x = h.detach().requires_grad_(True)
     blk(x, g).backward(torch.ones(h.size(0), 96, device=dev))
 
@@ -52,8 +53,14 @@ def ours_fwd():
 print("sageblock fwd+bwd (graph cached) ms", tm(ours))
 print("sageblock fwd only ms", tm(ours_fwd))
 print("torch ops fwd+bwd ms", bench.torch_ops_gpu_baseline(blk, ei, h, torch.ones(h.size(0), 96, device=dev), 3, 20) * 1e3)
-from torch.profiler import ProfilerActivity, profile  # noqa: E402
-with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+import cProfile  # noqa: E402
+import pstats  # noqa: E402
+
+torch.autograd.set_multithreading_enabled(False)     # backward on this thread: profiled
+pr = cProfile.Profile()
+pr.enable()
+for _ in range(50):
     ours()
-    torch.cuda.synchronize()
-print(prof.key_averages().table(sort_by="cpu_time_total", row_limit=25))
+torch.cuda.synchronize()
+pr.disable()
+pstats.Stats(pr).sort_stats("tottime").print_stats(40)
