@@ -36,6 +36,7 @@
 namespace {
 
 typedef float f4v __attribute__((ext_vector_type(4)));
+typedef short s8b __attribute__((ext_vector_type(8)));   // 8 x bf16 (MFMA operand)
 
 __device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -159,6 +160,174 @@ __global__ __launch_bounds__(64 * NW) void gru_fwd_kernel(
   }
 }
 
+// Forward with the recurrent product h W_hh^T on bf16 MFMAs in split form
+// ("bf16x3"): every fp32 operand x is carried as hi = bf16(x) plus
+// lo = bf16(x - hi) (16 significant bits of 24), and a product as
+// a_hi b_hi + a_hi b_lo + a_lo b_hi in fp32 accumulation -- the dropped
+// a_lo b_lo and the split remainders are ~2^-16 relative, ~1e-5 on a gate's
+// pre-activation (the GRU parity tests hold outputs and gradients to 1e-4
+// against the fp32 oracle).  v_mfma_f32_16x16x32_bf16 does a 32-deep k-step in
+// 16 cycles where the exact fp32 MFMA needs eight 16x16x4 steps of 32 cycles:
+// the recurrence's MFMA time drops ~5x (3 k-steps x 3 products x 3 gates per
+// step at H = 96, against 72 fp32 MFMAs).  The input product x W_ih^T (K <= 16)
+// stays on the exact fp32 MFMA.  Layout: lane (c, g4) holds W_hh rows g H + j
+// at k = 32 s + 8 g4 + e (e < 8) as the B operand, hi and lo (the same 72
+// VGPRs as the fp32 kernel at H = 96); h_t sits in LDS as an fp32 image in the
+// 16x16x32 A-operand layout and each reader splits its fragment.  Gate math,
+// stores and the gates workspace are gru_fwd_kernel's.
+__device__ __forceinline__ void split_bf16x8(const float (&v)[8], s8b& hi, s8b& lo) {
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t ph = sldm::pack_bf16x2(v[2 * e], v[2 * e + 1]);
+    h[e] = ph;
+    l[e] = sldm::pack_bf16x2(v[2 * e] - sldm::bf16_lo(ph), v[2 * e + 1] - sldm::bf16_hi(ph));
+  }
+  hi = __builtin_bit_cast(s8b, make_uint4(h[0], h[1], h[2], h[3]));
+  lo = __builtin_bit_cast(s8b, make_uint4(l[0], l[1], l[2], l[3]));
+}
+// Gate nonlinearities of the split kernel on the hardware transcendentals
+// (v_exp_f32, v_rcp_f32: ~1e-7 relative, far inside the 1e-4 bar): the
+// libm expf / tanhf / division sequences were the longest part of a step.
+__device__ __forceinline__ float fast_sigm(float v) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+}
+__device__ __forceinline__ float fast_tanh(float v) { return 2.0f * fast_sigm(2.0f * v) - 1.0f; }
+__device__ __forceinline__ f4v mfma32(s8b a, s8b b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// fp32 A-layout image of a [16 rows][KS*32] operand: element (row, k) of
+// k-step s = k >> 5 sits in lane row + 16 ((k & 31) >> 3), slot k & 7.
+__device__ __forceinline__ int aimg32(int row, int k) {
+  return (((k >> 5) * 64 + row + 16 * ((k & 31) >> 3)) << 3) + (k & 7);
+}
+
+template <int NW, int KI>
+__global__ __launch_bounds__(64 * NW) void gru_fwd_x3_kernel(
+    const float* __restrict__ x, int64_t ldxn, int64_t ldxt, int64_t N, int T, int I,
+    const float* __restrict__ w_ih, const float* __restrict__ w_hh,
+    const float* __restrict__ b_ih, const float* __restrict__ b_hh,
+    const float* __restrict__ h0, float* __restrict__ out, int64_t ldon, int64_t ldot,
+    float* __restrict__ h_n, float* __restrict__ gates) {
+  constexpr int H = 16 * NW;
+  constexpr int KS = (H + 31) / 32;         // 32-deep bf16 k-steps over the hidden dim
+  constexpr int IMG = KS * 64 * 8;          // floats per image
+  __shared__ __attribute__((aligned(16))) float himg[2][IMG];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int c = lane & 15, g4 = lane >> 4;
+  const int j = 16 * w + c;
+  const int64_t r0 = (int64_t)blockIdx.x * 16;
+
+  s8b whi[3][KS], wlo[3][KS];
+  float wih[3][KI];
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = 32 * s + 8 * g4 + e;
+        v[e] = k < H ? w_hh[(int64_t)(g * H + j) * H + k] : 0.f;
+      }
+      split_bf16x8(v, whi[g][s], wlo[g][s]);
+    }
+#pragma unroll
+    for (int q = 0; q < KI; ++q) {
+      const int k = 4 * q + g4;
+      wih[g][q] = k < I ? w_ih[(int64_t)(g * H + j) * I + k] : 0.f;
+    }
+  }
+  float bias[4];
+  bias[0] = (b_ih ? b_ih[j] : 0.f) + (b_hh ? b_hh[j] : 0.f);
+  bias[1] = (b_ih ? b_ih[H + j] : 0.f) + (b_hh ? b_hh[H + j] : 0.f);
+  bias[2] = b_ih ? b_ih[2 * H + j] : 0.f;
+  bias[3] = b_hh ? b_hh[2 * H + j] : 0.f;
+
+  if constexpr (H % 32 != 0) {              // zero k-padding of both images
+    for (int e = threadIdx.x; e < 2 * IMG; e += 64 * NW) (&himg[0][0])[e] = 0.f;
+    __syncthreads();
+  }
+  float hp[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t row = r0 + 4 * g4 + r;
+    hp[r] = (h0 && row < N) ? h0[row * H + j] : 0.f;
+    himg[0][aimg32(4 * g4 + r, j)] = hp[r];
+  }
+  const int64_t xrow = min(r0 + c, N - 1);
+  auto load_x = [&](int t, float (&xa)[KI]) {
+#pragma unroll
+    for (int q = 0; q < KI; ++q) {
+      const int k = 4 * q + g4;
+      xa[q] = (k < I && t < T) ? x[xrow * ldxn + (int64_t)t * ldxt + k] : 0.f;
+    }
+  };
+  float xa[KI], xn[KI];
+  load_x(0, xa);
+  __syncthreads();
+
+  for (int t = 0; t < T; ++t) {
+    load_x(t + 1, xn);
+    const float* hi = himg[t & 1];
+    f4v ar = {0.f, 0.f, 0.f, 0.f}, az = ar, an = ar, ahn = ar;
+#pragma unroll
+    for (int q = 0; q < KI; ++q) {
+      ar = mfma4(xa[q], wih[0][q], ar);
+      az = mfma4(xa[q], wih[1][q], az);
+      an = mfma4(xa[q], wih[2][q], an);
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const f4v* src = reinterpret_cast<const f4v*>(hi + ((s * 64 + lane) << 3));
+      const f4v u0 = src[0], u1 = src[1];
+      const float v[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+      s8b ahi, alo;
+      split_bf16x8(v, ahi, alo);
+      ar = mfma32(alo, whi[0][s], ar);
+      az = mfma32(alo, whi[1][s], az);
+      ahn = mfma32(alo, whi[2][s], ahn);
+      ar = mfma32(ahi, wlo[0][s], ar);
+      az = mfma32(ahi, wlo[1][s], az);
+      ahn = mfma32(ahi, wlo[2][s], ahn);
+      ar = mfma32(ahi, whi[0][s], ar);
+      az = mfma32(ahi, whi[1][s], az);
+      ahn = mfma32(ahi, whi[2][s], ahn);
+    }
+    float* ho = himg[(t + 1) & 1];
+    f4v gr, gz, gn, gh;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float rr = fast_sigm(ar[r] + bias[0]);
+      const float zz = fast_sigm(az[r] + bias[1]);
+      const float hn = ahn[r] + bias[3];
+      const float nn = fast_tanh(an[r] + bias[2] + rr * hn);
+      const float hv = (hp[r] - nn) * zz + nn;
+      gr[r] = rr; gz[r] = zz; gn[r] = nn; gh[r] = hn;
+      hp[r] = hv;
+      ho[aimg32(4 * g4 + r, j)] = hv;
+      const int64_t row = r0 + 4 * g4 + r;
+      if (row < N) out[row * ldon + (int64_t)t * ldot + j] = hv;
+    }
+    if (gates) {
+      f4v* gp = reinterpret_cast<f4v*>(gates) +
+                ((((int64_t)t * gridDim.x + blockIdx.x) * NW + w) * 4) * 64 + lane;
+      gp[0] = gr; gp[64] = gz; gp[128] = gn; gp[192] = gh;
+    }
+#pragma unroll
+    for (int q = 0; q < KI; ++q) xa[q] = xn[q];
+    __syncthreads();
+  }
+  if (h_n) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = r0 + 4 * g4 + r;
+      if (row < N) h_n[row * H + j] = hp[r];
+    }
+  }
+}
+
 // Backward.  Per step (t descending), wave w, lane (c, g4), rows 4 g4 + r:
 //   dh   = carry + dout[t]           (carry = dh_n at t = T-1)
 //   dn   = dh (1 - z),  dz = dh (h_{t-1} - n),  dh_{t-1} <- dh z
@@ -221,19 +390,40 @@ __global__ __launch_bounds__(64 * NW) void gru_bwd_kernel(
     }
   };
 
-  for (int t = T - 1; t >= 0; --t) {
-    const int b = t & 1;
+  // Step operands (saved gates, h_{t-1}, dout[t], x[t]) are loaded one step
+  // ahead: the loads of step t-1 are in flight while step t computes, instead
+  // of every step starting with a dependent global round trip.
+  struct StepIn {
+    f4v gr, gz, gn, gh;
+    float hp[4], go[4], xb[4];
+  };
+  auto load_step = [&](int t, StepIn& in) {
     const f4v* gp = reinterpret_cast<const f4v*>(gates) +
                     ((((int64_t)t * gridDim.x + blockIdx.x) * NW + w) * 4) * 64 + lane;
-    const f4v gr = gp[0], gz = gp[64], gn = gp[128], gh = gp[192];
-    float hp[4], xb[4];
+    in.gr = gp[0]; in.gz = gp[64]; in.gn = gp[128]; in.gh = gp[192];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t row = min(r0 + 4 * g4 + r, N - 1);
-      hp[r] = t > 0 ? out[row * ldon + (int64_t)(t - 1) * ldot + j] : (h0 ? h0[row * H + j] : 0.f);
-      if (dout && live[r]) dh[r] += dout[row * lddn + (int64_t)t * lddt + j];
+      in.hp[r] = t > 0 ? out[row * ldon + (int64_t)(t - 1) * ldot + j]
+                       : (h0 ? h0[row * H + j] : 0.f);
+      in.go[r] = (dout && live[r]) ? dout[row * lddn + (int64_t)t * lddt + j] : 0.f;
     }
-    load_x(t, xb);
+    load_x(t, in.xb);
+  };
+  StepIn nxt;
+  load_step(T - 1, nxt);
+  for (int t = T - 1; t >= 0; --t) {
+    const int b = t & 1;
+    const StepIn cur = nxt;
+    if (t > 0) load_step(t - 1, nxt);
+    const f4v gr = cur.gr, gz = cur.gz, gn = cur.gn, gh = cur.gh;
+    float hp[4], xb[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      hp[r] = cur.hp[r];
+      xb[r] = cur.xb[r];
+      dh[r] += cur.go[r];
+    }
     f4v dar, daz, dan, dghn;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -384,14 +574,26 @@ __global__ __launch_bounds__(256) void gru_dx_kernel(const float* __restrict__ d
   dx[n * lddxn + t * lddxt + i] = s;
 }
 
+// The split-bf16 recurrent product (gru_fwd_x3_kernel) is the default;
+// SLDM_GRU_BF16X3=0 selects the exact fp32 MFMA kernel (read per call).
+bool gru_bf16x3_enabled() {
+  const char* e = getenv("SLDM_GRU_BF16X3");
+  return !(e && e[0] == '0');
+}
+
 template <int NW>
 int launch_fwd(int ki, dim3 grid, hipStream_t st, const float* x, int64_t ldxn, int64_t ldxt,
                int64_t N, int T, int I, const float* w_ih, const float* w_hh, const float* b_ih,
                const float* b_hh, const float* h0, float* out, int64_t ldon, int64_t ldot,
                float* h_n, float* gates) {
-#define SLDM_GRU_F(KI)                                                                       \
-  gru_fwd_kernel<NW, KI><<<grid, 64 * NW, 0, st>>>(x, ldxn, ldxt, N, T, I, w_ih, w_hh, b_ih, \
-                                                   b_hh, h0, out, ldon, ldot, h_n, gates)
+#define SLDM_GRU_F(KI)                                                                         \
+  if (gru_bf16x3_enabled())                                                                    \
+    gru_fwd_x3_kernel<NW, KI><<<grid, 64 * NW, 0, st>>>(x, ldxn, ldxt, N, T, I, w_ih, w_hh,    \
+                                                        b_ih, b_hh, h0, out, ldon, ldot, h_n, \
+                                                        gates);                               \
+  else                                                                                         \
+    gru_fwd_kernel<NW, KI><<<grid, 64 * NW, 0, st>>>(x, ldxn, ldxt, N, T, I, w_ih, w_hh, b_ih, \
+                                                     b_hh, h0, out, ldon, ldot, h_n, gates)
   switch (ki) {
     case 1: SLDM_GRU_F(1); break;
     case 2: SLDM_GRU_F(2); break;

@@ -1,7 +1,9 @@
 """The HIP GRU (sldm_sage.GRU, csrc/gru.hip) against torch.nn.GRU on the CPU
 (the reference's own op, grusage.py:66-71,160-161; pinned to the restatement
 oracle/gru_ref.py by tests/test_oracle.py): outputs, h_n and every gradient
-within 1e-4 (fp32), for the model's shape and the edge cases of the API."""
+within 1e-4 (fp32), for the model's shape and the edge cases of the API --
+with the forward's recurrent product in split-bf16 form (default) and on the
+exact fp32 MFMA."""
 from __future__ import annotations
 
 import pytest
@@ -9,6 +11,14 @@ import torch
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(autouse=True, params=["bf16x3", "fp32"])
+def gru_kernel(request, monkeypatch):
+    """Every test on both forward kernels: the split-bf16 recurrent product
+    (default) and the exact fp32 MFMA one (SLDM_GRU_BF16X3=0)."""
+    monkeypatch.setenv("SLDM_GRU_BF16X3", "1" if request.param == "bf16x3" else "0")
+    return request.param
 
 
 def _run_pair(N, T, I, H, batch_first=True, bias=True, h0=False, gout=True, gh=True,
