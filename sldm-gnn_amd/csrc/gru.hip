@@ -335,7 +335,7 @@ __global__ __launch_bounds__(64 * NW) void gru_fwd_x3_kernel(
 //   dGi  = [dar, daz, dan],  dGh = [dar, daz, dan r]
 //   dh_{t-1} += dGh W_hh                      (LDS image of dGh, W_hh frags)
 //   dW_hh += dGh^T h_{t-1}, dW_ih += dGi^T x_t, db += column sums
-template <int NW, int KI>
+template <int NW, int KI, bool X3>
 __global__ __launch_bounds__(64 * NW) void gru_bwd_kernel(
     const float* __restrict__ x, int64_t ldxn, int64_t ldxt, int64_t N, int T, int I,
     const float* __restrict__ w_hh, const float* __restrict__ h0,
@@ -359,10 +359,26 @@ __global__ __launch_bounds__(64 * NW) void gru_bwd_kernel(
   const int64_t r0 = (int64_t)blockIdx.x * 16;
 
   // B-fragments of dGh W_hh: B[k = gate column 4q + g4][col j] = W_hh[4q + g4][j]
+  // (X3: 32-deep k-steps, lane (c, g4) k = 32 s + 8 g4 + e, as bf16 hi | lo)
+  constexpr int KS3 = 3 * H / 32;           // X3 k-steps over the 3H gate columns
+  static_assert(!X3 || (3 * H) % 32 == 0, "split form: 3H a multiple of 32");
   float* wmine = wimg + (int64_t)w * KG * 64;
+  if constexpr (X3) {
+    uint4* wq = reinterpret_cast<uint4*>(wmine);
+    for (int s3 = 0; s3 < KS3; ++s3) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = w_hh[(int64_t)(32 * s3 + 8 * g4 + e) * H + j];
+      s8b hi, lo;
+      split_bf16x8(v, hi, lo);
+      wq[(s3 * 64 + lane) * 2] = __builtin_bit_cast(uint4, hi);
+      wq[(s3 * 64 + lane) * 2 + 1] = __builtin_bit_cast(uint4, lo);
+    }
+  } else {
 #pragma unroll 4
-  for (int q = 0; q < KG; ++q)
-    wmine[((q >> 2) * 64 + lane) * 4 + (q & 3)] = w_hh[(int64_t)(4 * q + g4) * H + j];
+    for (int q = 0; q < KG; ++q)
+      wmine[((q >> 2) * 64 + lane) * 4 + (q & 3)] = w_hh[(int64_t)(4 * q + g4) * H + j];
+  }
 
   f4v dwh[3][NW], dwi[3];
 #pragma unroll
@@ -442,9 +458,15 @@ __global__ __launch_bounds__(64 * NW) void gru_bwd_kernel(
       db[2] += dan[r];
       db[3] += dghn[r];
       // dGh image (A-fragments over the 3H gate columns) and h_{t-1} tile
-      gimg[b][aimg(4 * g4 + r, j)] = dar[r];
-      gimg[b][aimg(4 * g4 + r, H + j)] = daz[r];
-      gimg[b][aimg(4 * g4 + r, 2 * H + j)] = dghn[r];
+      if constexpr (X3) {
+        gimg[b][aimg32(4 * g4 + r, j)] = dar[r];
+        gimg[b][aimg32(4 * g4 + r, H + j)] = daz[r];
+        gimg[b][aimg32(4 * g4 + r, 2 * H + j)] = dghn[r];
+      } else {
+        gimg[b][aimg(4 * g4 + r, j)] = dar[r];
+        gimg[b][aimg(4 * g4 + r, H + j)] = daz[r];
+        gimg[b][aimg(4 * g4 + r, 2 * H + j)] = dghn[r];
+      }
     }
     *reinterpret_cast<f4v*>(&pimg[b][(w * 64 + lane) * 4]) = f4v{hp[0], hp[1], hp[2], hp[3]};
     if (dgi) {                              // dx needs dGi: [N, T, 3H] in (row, t) order
@@ -463,12 +485,29 @@ __global__ __launch_bounds__(64 * NW) void gru_bwd_kernel(
     // dh_{t-1} += dGh W_hh (rows 4 g4 + r, column j)
     f4v acc = {0.f, 0.f, 0.f, 0.f};
     const float* gi = gimg[b];
+    if constexpr (X3) {
+      const uint4* wq = reinterpret_cast<const uint4*>(wmine);
 #pragma unroll
-    for (int qq = 0; qq < KG / 4; ++qq) {
-      const f4v a4 = *reinterpret_cast<const f4v*>(gi + (qq * 64 + lane) * 4);
-      const f4v b4 = *reinterpret_cast<const f4v*>(wmine + (qq * 64 + lane) * 4);
+      for (int s3 = 0; s3 < KS3; ++s3) {
+        const f4v* src = reinterpret_cast<const f4v*>(gi + ((s3 * 64 + lane) << 3));
+        const f4v u0 = src[0], u1 = src[1];
+        const float v[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+        s8b ahi, alo;
+        split_bf16x8(v, ahi, alo);
+        const s8b bhi = __builtin_bit_cast(s8b, wq[(s3 * 64 + lane) * 2]);
+        const s8b blo = __builtin_bit_cast(s8b, wq[(s3 * 64 + lane) * 2 + 1]);
+        acc = mfma32(alo, bhi, acc);
+        acc = mfma32(ahi, blo, acc);
+        acc = mfma32(ahi, bhi, acc);
+      }
+    } else {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc = mfma4(a4[u], b4[u], acc);
+      for (int qq = 0; qq < KG / 4; ++qq) {
+        const f4v a4 = *reinterpret_cast<const f4v*>(gi + (qq * 64 + lane) * 4);
+        const f4v b4 = *reinterpret_cast<const f4v*>(wmine + (qq * 64 + lane) * 4);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = mfma4(a4[u], b4[u], acc);
+      }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) dh[r] += acc[r];
@@ -533,8 +572,15 @@ __global__ __launch_bounds__(256) void gru_reduce_kernel(const float* __restrict
   const int64_t stride = 3 * H * H + 3 * H * 16 + 4 * H;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= stride) return;
-  float s = 0.f;
-  for (int64_t p = 0; p < nparts; ++p) s += part[p * stride + e];
+  // eight interleaved partial chains (loads in flight), then combined in a
+  // fixed order: deterministic
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int64_t p = 0;
+  for (; p + 8 <= nparts; p += 8)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += part[(p + u) * stride + e];
+  for (; p < nparts; ++p) a[0] += part[p * stride + e];
+  const float s = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   if (e < 3 * H * H) {
     dw_hh[e] = s;
     return;
@@ -613,7 +659,12 @@ int launch_bwd(dim3 grid, hipStream_t st, const float* x, int64_t ldxn, int64_t 
   constexpr int H = 16 * NW;
   constexpr size_t lds = sizeof(float) * (2 * (3 * H / 4) * 64 + 2 * NW * 256 + 3 * H * H);
   static_assert(lds <= 160 * 1024, "GRU backward LDS budget");
-  auto kern = gru_bwd_kernel<NW, 1>;
+  // the split form needs the 3H gate columns in whole 32-deep k-steps
+  // (H = 32, 64, 96); other sizes run the fp32 MFMA recurrence
+  auto kern = gru_bwd_kernel<NW, 1, false>;
+  if constexpr ((3 * H) % 32 == 0) {
+    if (gru_bf16x3_enabled()) kern = gru_bwd_kernel<NW, 1, true>;
+  }
   SLDM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   kern<<<grid, 64 * NW, lds, st>>>(x, ldxn, ldxt, N, T, I, w_hh, h0, out, ldon, ldot, gates,
