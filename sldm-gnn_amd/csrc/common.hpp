@@ -261,6 +261,33 @@ __device__ __forceinline__ float row4_sum(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// Split-bf16 operands ("bf16x3" products): x = hi + lo with hi = bf16(x),
+// lo = bf16(x - hi) (16 significant bits of fp32's 24); a product as
+// a_hi b_hi + a_hi b_lo + a_lo b_hi on v_mfma_f32_16x16x32_bf16 in fp32
+// accumulation is within ~2^-16 relative of the fp32 product.
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void split_bf16x8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t ph = pack_bf16x2(v[2 * e], v[2 * e + 1]);
+    h[e] = ph;
+    l[e] = pack_bf16x2(v[2 * e] - bf16_lo(ph), v[2 * e + 1] - bf16_hi(ph));
+  }
+  hi = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+  lo = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+}
+// 4 floats -> (hi, lo) as two packed bf16x4 words (uint2 each)
+__device__ __forceinline__ void split_bf16x4(const float (&v)[4], uint2& hi, uint2& lo) {
+  const uint32_t h0 = pack_bf16x2(v[0], v[1]), h1 = pack_bf16x2(v[2], v[3]);
+  hi = make_uint2(h0, h1);
+  lo = make_uint2(pack_bf16x2(v[0] - bf16_lo(h0), v[1] - bf16_hi(h0)),
+                  pack_bf16x2(v[2] - bf16_lo(h1), v[3] - bf16_hi(h1)));
+}
+// fp32 dense GEMMs on split-bf16 MFMAs (gemm.hip's NT weight-stationary
+// kernel), opt-in with SLDM_FP32_GEMM=split; default: exact fp32 MFMA.
+bool fp32_gemm_split();
+
 // Big-tile bf16 dense kernels (gemm_big.hip); the gemm.hip entry points route
 // conforming shapes to them.  SLDM_BIG_GEMM=0 in the environment disables them
 // (A/B comparisons against the 64-row kernels).

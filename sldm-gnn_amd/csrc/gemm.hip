@@ -504,6 +504,129 @@ __global__ __launch_bounds__(kBlock, 2) void gemm_nt_ws32_kernel(NtArgs<float> p
   }
 }
 
+// The same weight-stationary NT kernel with split-bf16 products (fp32 in and
+// out, fp32 accumulation): the weights are split once into hi / lo bf16
+// B-fragments (32-deep k-steps: the same VGPR count as the fp32 fragments), A
+// tiles are split while they are staged into LDS (hi and lo bf16 images), and
+// each 32-deep k-step is three v_mfma_f32_16x16x32_bf16 (lo·hi, hi·lo, hi·hi)
+// where the exact kernel issues eight 16x16x4 fp32 MFMAs of twice the cycles.
+// ~2^-16 relative per product; the epilogue is the exact kernel's.
+template <int TPW, int KC, int MODE>
+__global__ __launch_bounds__(kBlock, 2) void gemm_nt_ws32x3_kernel(NtArgs<float> p,
+                                                                    int64_t ntiles) {
+  constexpr int MT = 2, BM = 32;
+  constexpr int KS3 = KC / 32;              // 32-deep k-steps
+  constexpr int VPR = KC / 4;               // 16-B fp32 vectors per A row
+  constexpr int NV = BM * VPR / kBlock;
+  constexpr int PB = 2 * KC + 16;           // bf16 image row pitch (bytes)
+  static_assert(BM * VPR % kBlock == 0 && KC % 32 == 0, "ws32x3 shape");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* img_hi = reinterpret_cast<char*>(smem);
+  char* img_lo = img_hi + BM * PB;
+  float* lds_c = reinterpret_cast<float*>(img_lo + BM * PB);
+  const int ldc = 16 * p.ct + 4;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q = lane >> 4, r16 = lane & 15;
+
+  int64_t tile = blockIdx.x;
+  if (tile >= ntiles) return;
+
+  bool tval[TPW];
+  s8v whi[KS3][TPW], wlo[KS3][TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int tid = wave + 4 * t;
+    tval[t] = tid < p.ct;
+    const int c = 16 * tid + r16;
+    const int bc = c < p.Nc ? c : p.Nc - 1;
+#pragma unroll
+    for (int ks = 0; ks < KS3; ++ks) {
+      const f4v u0 = nt_load_b<float, true>(p, bc, 32 * ks + 8 * q);
+      const f4v u1 = nt_load_b<float, true>(p, bc, 32 * ks + 8 * q + 4);
+      const float v[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+      sldm::split_bf16x8(v, whi[ks][t], wlo[ks][t]);
+    }
+  }
+
+  f4v st[NV];
+  auto load_tile = [&](int64_t tl) {
+    const int64_t m0 = tl * BM;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = threadIdx.x + i * kBlock;
+      const int r = v / VPR, kv = (v - r * VPR) * 4;
+      const int64_t row = min(m0 + r, p.M - 1);
+      const float* src = kv < p.k0 ? p.a0 + row * p.lda0 + kv : p.a1 + row * p.lda1 + (kv - p.k0);
+      st[i] = *reinterpret_cast<const f4v*>(src);
+    }
+  };
+  load_tile(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = threadIdx.x + i * kBlock;
+      const int r = v / VPR, kv = (v - r * VPR) * 4;
+      const float f[4] = {st[i][0], st[i][1], st[i][2], st[i][3]};
+      uint2 h, l;
+      sldm::split_bf16x4(f, h, l);
+      *reinterpret_cast<uint2*>(img_hi + r * PB + 2 * kv) = h;
+      *reinterpret_cast<uint2*>(img_lo + r * PB + 2 * kv) = l;
+    }
+    __syncthreads();
+    if (tile + gridDim.x < ntiles) load_tile(tile + gridDim.x);
+
+    f4v acc[MT][TPW];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) acc[m][t] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS3; ++ks) {
+      s8v ahi[MT], alo[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int off = (16 * m + r16) * PB + 64 * ks + 16 * q;
+        ahi[m] = *reinterpret_cast<const s8v*>(img_hi + off);
+        alo[m] = *reinterpret_cast<const s8v*>(img_lo + off);
+      }
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        if (!tval[t]) continue;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[m], whi[ks][t], acc[m][t], 0, 0, 0);
+          acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[m], wlo[ks][t], acc[m][t], 0, 0, 0);
+          acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[m], whi[ks][t], acc[m][t], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      if (!tval[t]) continue;
+      const int c = 16 * (wave + 4 * t) + r16;
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lds_c[(16 * m + 4 * q + r) * ldc + c] = acc[m][t][r];
+    }
+    __syncthreads();
+    nt_row_epilogue<float, MODE>(p, lds_c, ldc, tile * BM, 0, BM, wave, lane);
+  }
+}
+
+template <int TP, int KCV, int MODE>
+int launch_ws32x3_t(const NtArgs<float>& p, int64_t ntiles, int64_t grid, hipStream_t stream) {
+  const size_t lds = (size_t)2 * 32 * (2 * KCV + 16) + sizeof(float) * 32 * (size_t)(16 * p.ct + 4);
+  auto kern = gemm_nt_ws32x3_kernel<TP, KCV, MODE>;
+  if (lds > 65536)
+    SLDM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  kern<<<(unsigned)grid, kBlock, lds, stream>>>(p, ntiles);
+  SLDM_LAUNCH_CHECK("gemm_nt_ws32x3_kernel");
+  return SLDM_OK;
+}
+
 template <int TP, int KCV, int MODE>
 int launch_ws32_t(const NtArgs<float>& p, int64_t ntiles, int64_t grid, size_t lds,
                   hipStream_t stream) {
@@ -528,6 +651,14 @@ int launch_nt_ws32(const NtArgs<float>& p, int tpw, hipStream_t stream) {
     return -1;
   const int64_t ntiles = (p.M + 31) / 32;
   const int64_t grid = ntiles < 512 ? ntiles : 512;   // 2 blocks x 256 CUs, persistent
+  if (sldm::fp32_gemm_split()) {
+    if (p.K == 256 && tpw == 1) return launch_ws32x3_t<1, 256, MODE>(p, ntiles, grid, stream);
+    if (p.K == 256 && tpw == 2) return launch_ws32x3_t<2, 256, MODE>(p, ntiles, grid, stream);
+    if (p.K == 128 && tpw == 1) return launch_ws32x3_t<1, 128, MODE>(p, ntiles, grid, stream);
+    if (p.K == 128 && tpw == 2) return launch_ws32x3_t<2, 128, MODE>(p, ntiles, grid, stream);
+    if (p.K == 128 && tpw == 3) return launch_ws32x3_t<3, 128, MODE>(p, ntiles, grid, stream);
+    if (p.K == 128 && tpw == 4) return launch_ws32x3_t<4, 128, MODE>(p, ntiles, grid, stream);
+  }
   const size_t lds = sizeof(float) * (32 * (size_t)(p.K + 4) + 32 * (size_t)(16 * p.ct + 4));
   if (p.K == 256 && tpw == 1) return launch_ws32_t<1, 256, MODE>(p, ntiles, grid, lds, stream);
   if (p.K == 256 && tpw == 2) return launch_ws32_t<2, 256, MODE>(p, ntiles, grid, lds, stream);
@@ -1011,3 +1142,14 @@ extern "C" int sldm_gemm_tn(int dtype, const void* a, int64_t lda, int64_t mo, c
   };
   return dtype == SLDM_F32 ? run((float*)nullptr) : run((uint16_t*)nullptr);
 }
+
+namespace sldm {
+// Opt-in (SLDM_FP32_GEMM=split): the split form is ~2^-16 relative per
+// product, which flips LeakyReLU branches of pre-activations within ~1e-5 of
+// zero against the fp32 oracle; the exact kernels (~1e-7) stay the default.
+// Read per call so tests can compare both forms in one process.
+bool fp32_gemm_split() {
+  const char* e = getenv("SLDM_FP32_GEMM");
+  return e && e[0] == 's';
+}
+}  // namespace sldm

@@ -175,17 +175,7 @@ __global__ __launch_bounds__(64 * NW) void gru_fwd_kernel(
 // VGPRs as the fp32 kernel at H = 96); h_t sits in LDS as an fp32 image in the
 // 16x16x32 A-operand layout and each reader splits its fragment.  Gate math,
 // stores and the gates workspace are gru_fwd_kernel's.
-__device__ __forceinline__ void split_bf16x8(const float (&v)[8], s8b& hi, s8b& lo) {
-  uint32_t h[4], l[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const uint32_t ph = sldm::pack_bf16x2(v[2 * e], v[2 * e + 1]);
-    h[e] = ph;
-    l[e] = sldm::pack_bf16x2(v[2 * e] - sldm::bf16_lo(ph), v[2 * e + 1] - sldm::bf16_hi(ph));
-  }
-  hi = __builtin_bit_cast(s8b, make_uint4(h[0], h[1], h[2], h[3]));
-  lo = __builtin_bit_cast(s8b, make_uint4(l[0], l[1], l[2], l[3]));
-}
+using sldm::split_bf16x8;
 // Gate nonlinearities of the split kernel on the hardware transcendentals
 // (v_exp_f32, v_rcp_f32: ~1e-7 relative, far inside the 1e-4 bar): the
 // libm expf / tanhf / division sequences were the longest part of a step.

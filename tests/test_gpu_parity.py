@@ -843,16 +843,24 @@ def test_fp32_ws32_nt_bit_exact_vs_tile(m, f, monkeypatch):
     dh = torch.randn(m, f, generator=gen, device=DEV)
     wt = torch.randn(2 * f, f, generator=gen, device=DEV) / f ** 0.5
 
-    def run(ws):
+    def run(ws, mode="exact"):
         monkeypatch.setenv("SLDM_NT_WS32", "1" if ws else "0")
+        monkeypatch.setenv("SLDM_FP32_GEMM", mode)
         fwd = ops.sage_dense_fwd(agg, x, wcat, b, gam, bet, 1e-5, 0.1, 0.25, 5, True)
         dx = ops.gemm_nt_rowscale(dh, wt, g.rowptr, f)
         dxs = ops.gemm_nt_rowscale(dh, wt, g.rowptr, f, split=True)
         torch.cuda.synchronize()
         return [*fwd, dx, *dxs]
 
-    for a, c in zip(run(True), run(False)):
+    exact = run(True)
+    for a, c in zip(exact, run(False)):
         assert torch.equal(a, c)
+    # the split-bf16 form of the same kernel (opt-in SLDM_FP32_GEMM=split):
+    # same dropout mask, within ~2^-16 relative of the exact products
+    split = run(True, "split")
+    assert torch.equal(split[0] != 0, exact[0] != 0)
+    for a, c in zip(split, exact):
+        torch.testing.assert_close(a, c, atol=1e-4, rtol=1e-4)
 
 
 # ------------------------------------------------ overlapped (split) gather --
