@@ -27,6 +27,7 @@ step / 8 TB/s + the step's GEMM FLOP / the dense MFMA peak, as T*/t_step.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import statistics
@@ -54,6 +55,7 @@ ZIPF_A = 0.47   # dst rank ~ k^-a over N ranks: max in-degree ~ E*(2^(1-a)-1)/(N
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HBM_COPY_GBS = 6290.0   # measured float4-copy ceiling (MI355X_MICROARCH.md)
 MFMA_PEAK_TFLOPS = {torch.bfloat16: 2500.0, torch.float32: 157.3}   # dense, same guide
+BREAKDOWN_STEPS = 2      # untimed steps with every op bracketed (the "kernels" table)
 PMC_SUMMARY = "r2b_c4_pmc_traffic.json"   # latest committed PMC passes (tools/profile_round.sh)
 
 
@@ -252,11 +254,16 @@ def _time_steps(step, warmup, steps):
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / steps
+    gc.collect()
+    gc.disable()        # as timeit does: no collector pauses inside the timed steps
+    try:
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps
+    finally:
+        gc.enable()
 
 
 def bench_vehicle(args, dev):
@@ -572,8 +579,14 @@ def main():
         timer = KernelTimer()
         barrier()
         if timed_kernels:
-            ops.set_timing_hook(timer)
+            # inside the timed region only the roofline kernel is bracketed
+            # with HIP events (per-op events on every launch cost the small
+            # configurations up to 40 % of a step); the per-kernel table comes
+            # from the untimed breakdown steps below
+            ops.set_timing_hook(timer, names={"gather_fwd"})
         marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        gc.collect()
+        gc.disable()        # as timeit does: no collector pauses inside the timed steps
         t0 = time.perf_counter()
         marks[0].record()
         for i in range(args.steps):
@@ -582,6 +595,7 @@ def main():
             marks[i + 1].record()
         barrier()
         elapsed = time.perf_counter() - t0
+        gc.enable()
         step_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)]
         ops.set_timing_hook(None)
         if world > 1:
@@ -589,6 +603,18 @@ def main():
             tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
             all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
             elapsed = tt.item()
+
+        kern_all = {}
+        if timed_kernels:
+            # untimed breakdown: every op bracketed, BREAKDOWN_STEPS steps
+            t_all = KernelTimer()
+            ops.set_timing_hook(t_all)
+            for _ in range(BREAKDOWN_STEPS):
+                blk.zero_grad(set_to_none=True)
+                step()
+            ops.set_timing_hook(None)
+            barrier()
+            kern_all = t_all.summary()
 
         # CSR-build-inclusive step (N=1: static-graph cache cleared once)
         incl = None
@@ -600,22 +626,22 @@ def main():
             step()
             barrier()
             incl = e * L / (time.perf_counter() - t1)
-        return elapsed, timer.summary(), dist_info, incl, step_ms
+        return elapsed, timer.summary(), dist_info, incl, step_ms, kern_all
 
-    elapsed, kern, dist_info, incl, step_ms = run(args.graph, True)
+    elapsed, kern_timed, dist_info, incl, step_ms, kern = run(args.graph, True)
     variant = None
     if world > 1 and args.graph == "uniform":
         # also the locality-structured variant (block-community
         # graph, cut fraction stated) -- the regime where the exchange overlaps.
         torch.cuda.empty_cache()
-        v_el, _, v_info, _, _ = run("local", False)
+        v_el, _, v_info, _, _, _ = run("local", False)
         variant = dict(graph="local", value=round(e * L * args.steps / v_el, 1),
                        ms_per_step=round(v_el / args.steps * 1e3, 3), **v_info)
         torch.cuda.empty_cache()
 
     ms = elapsed / args.steps * 1e3
     value = e * L * args.steps / elapsed
-    g = kern.get("gather_fwd")
+    g = kern_timed.get("gather_fwd")
     roof = None
     if g:
         achieved = g["avg_bytes"] / (g["avg_ms"] * 1e-3) / 1e9
@@ -638,7 +664,7 @@ def main():
     # SURVEY.md §8d full-step roofline: T* = (algorithmic bytes of every timed
     # kernel in a step) / HBM peak + (GEMM FLOP of a step) / dense MFMA peak,
     # reported as T*/t (N = 1; at N > 1 the per-rank work is not the whole graph).
-    step_bytes = sum(v["avg_bytes"] * v["launches"] for v in kern.values()) / args.steps
+    step_bytes = sum(v["avg_bytes"] * v["launches"] for v in kern.values()) / BREAKDOWN_STEPS
     step_roof = None
     if kern and not use_dist:
         flop = 3 * 2.0 * n * 2 * f * f * L        # fwd, dX, dW of [N,2F]x[2F,F] per layer
@@ -701,6 +727,9 @@ def main():
             "step_roofline": step_roof,
             "roofline": roof,
             "kernels": kernels,
+            "kernels_from": (f"{BREAKDOWN_STEPS} untimed steps after the timed region, HIP events "
+                             "around every launch (inside the timed region only the roofline "
+                             "kernel's launches carry events)"),
             "cpu_baseline": base,
             "torch_ops_gpu_baseline": torch_gpu,
         }

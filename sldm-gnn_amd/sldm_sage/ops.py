@@ -17,9 +17,15 @@ _DTYPE_CODE = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16}
 _timing_hook = None
 
 
-def set_timing_hook(hook) -> None:
-    global _timing_hook
+_timing_names = None
+
+
+def set_timing_hook(hook, names=None) -> None:
+    """Bracket launches with HIP events and hand them to ``hook`` (bench.py);
+    ``names``: only these ops (None: all).  Diagnostic plumbing."""
+    global _timing_hook, _timing_names
     _timing_hook = hook
+    _timing_names = None if names is None else frozenset(names)
 
 
 def dtype_code(t: torch.Tensor) -> int:
@@ -71,7 +77,7 @@ class _Timed:
         self.name, self.units, self.start = name, units, None
 
     def __enter__(self):
-        if _timing_hook is not None:
+        if _timing_hook is not None and (_timing_names is None or self.name in _timing_names):
             self.start = torch.cuda.Event(enable_timing=True)
             self.start.record()
         return self
