@@ -903,8 +903,8 @@ def measure_link_bps(device: torch.device, group=None, per_peer_bytes: int = 32 
     world = dist.get_world_size(group)
     if world < 2 or dist.get_backend(group) != "nccl" or device.type != "cuda":
         return None
-    n = per_peer_bytes // 2
-    inp = torch.empty(world * n, dtype=torch.bfloat16, device=device).normal_()
+    n = per_peer_bytes // 4
+    inp = torch.empty(world * n, dtype=torch.float32, device=device).normal_()
     out = torch.empty_like(inp)
     dist.all_to_all_single(out, inp, group=group)          # warm-up (connections)
     torch.cuda.synchronize(device)
