@@ -465,6 +465,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     use_dist = world > 1 or args.force_dist
+    t_start = time.perf_counter()
+
+    def progress(msg):
+        # rank 0's progress on stderr (the JSON line stays the only stdout line)
+        if rank == 0 and use_dist:
+            free, total = torch.cuda.mem_get_info()
+            print(f"[bench] {time.perf_counter() - t_start:7.1f} s  {msg}  [gpu free "
+                  f"{free / 2**30:.0f} of {total / 2**30:.0f} GiB, peak "
+                  f"{torch.cuda.max_memory_allocated() / 2**30:.1f} GiB]", file=sys.stderr,
+                  flush=True)
     if use_dist:
         import torch.distributed as dist
         # one GPU per rank (RCCL); a gloo rehearsal may put several ranks on one GPU
@@ -512,6 +522,7 @@ def main():
         """Build the workload on graph ``kind``, warm up, time args.steps steps
         (max over ranks).  Returns (elapsed_s, kernel summary, dist info, incl)."""
         ei, x = make_graph(n, e, f, dtype, dev, kind=kind)
+        progress(f"graph {kind} built")
         torch.manual_seed(0)
         blk = SageBlock([f] * (L + 1), dropout=0.25, negative_slope=0.1).to(dev).train()
         gout = torch.randn(n, f, device=dev, generator=torch.Generator(device=dev).manual_seed(2)
@@ -521,6 +532,7 @@ def main():
             from sldm_sage.dist import DistSageBlock, plan_partition
             part, plan = plan_partition(ei, n, world, rank, f, x.element_size(),
                                         strategy=args.strategy, link_bps=link_bps)
+            progress(f"partitioned: {plan['strategy']}")
             model = DistSageBlock(blk, part)
             x_in = x[part.row_begin:part.row_end].contiguous()
             g_in = gout[part.row_begin:part.row_end].contiguous()
@@ -576,6 +588,7 @@ def main():
         for _ in range(args.warmup):
             blk.zero_grad(set_to_none=True)
             step()
+        progress("warm-up done")
         timer = KernelTimer()
         barrier()
         if timed_kernels:
@@ -596,6 +609,7 @@ def main():
         barrier()
         elapsed = time.perf_counter() - t0
         gc.enable()
+        progress(f"timed steps done ({elapsed / args.steps * 1e3:.1f} ms/step)")
         step_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)]
         ops.set_timing_hook(None)
         if world > 1:

@@ -58,6 +58,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import os
+import sys
 import time
 
 import torch
@@ -206,6 +208,23 @@ def broadcast(t: torch.Tensor, src: int = 0, group=None) -> None:
 _ROW_COST_EDGES = 17.0
 
 
+_TRACE = os.environ.get("SLDM_DIST_TRACE") == "1"
+_T0 = time.perf_counter()
+
+
+def _trace(msg: str) -> None:
+    """Per-rank setup timing on stderr (SLDM_DIST_TRACE=1; diagnostics)."""
+    if _TRACE:
+        r = dist.get_rank() if dist.is_initialized() else 0
+        mem = ""
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            free, total = torch.cuda.mem_get_info()
+            mem = (f"  [gpu free {free / 2**30:.0f} of {total / 2**30:.0f} GiB,"
+                   f" reserved {torch.cuda.memory_reserved() / 2**30:.1f} GiB]")
+        print(f"[dist r{r}] {time.perf_counter() - _T0:8.2f} s  {msg}{mem}", file=sys.stderr,
+              flush=True)
+
+
 def row_bounds(edge_index: torch.Tensor, num_nodes: int, world: int,
                balance: str = "cost") -> list[int]:
     """[W+1] row offsets of the W contiguous row blocks (same on every rank:
@@ -216,14 +235,15 @@ def row_bounds(edge_index: torch.Tensor, num_nodes: int, world: int,
     if balance != "cost":
         raise ValueError(f"unknown balance {balance!r} (rows, cost)")
     dev = edge_index.device
-    w = torch.full((num_nodes,), _ROW_COST_EDGES, dtype=torch.float64, device=dev)
+    # integer costs (exact, and bincount's int64 atomics are native; fp64
+    # index_add_ was the slowest step of partitioning with ranks sharing a GPU)
+    w = torch.full((num_nodes,), int(_ROW_COST_EDGES), dtype=torch.int64, device=dev)
     if edge_index.numel():
-        ones = torch.ones(edge_index.size(1), dtype=torch.float64, device=dev)
-        w.index_add_(0, edge_index[1].long(), ones)
-        w.index_add_(0, edge_index[0].long(), ones)
+        w += torch.bincount(edge_index[1].long(), minlength=num_nodes)[:num_nodes]
+        w += torch.bincount(edge_index[0].long(), minlength=num_nodes)[:num_nodes]
     cum = torch.cumsum(w, 0)
-    total = float(cum[-1])
-    targets = torch.tensor([total * r / world for r in range(1, world)], dtype=torch.float64,
+    total = int(cum[-1])
+    targets = torch.tensor([total * r // world for r in range(1, world)], dtype=torch.int64,
                            device=dev)
     cuts = torch.searchsorted(cum, targets).tolist() if world > 1 else []
     bounds = [0] + [min(int(c) + 1, num_nodes) for c in cuts] + [num_nodes]
@@ -338,11 +358,16 @@ def _build_plan(ids: torch.Tensor, r0: int, r1: int, bounds: list[int], world: i
 
     Returns (remap, plan): remap(global ids) -> halo-buffer positions."""
     dev = ids.device
+    _trace("build_plan: unique")
     uniq = torch.unique(ids)                                   # sorted
+    _trace("build_plan: remote")
     remote = uniq[(uniq < r0) | (uniq >= r1)]                  # sorted => grouped by owner
     owner = _owner(remote, bounds)
+    _trace("build_plan: owner counts")
     need_counts = torch.bincount(owner, minlength=world)[:world].tolist()
+    _trace("build_plan: exchange counts")
     give_counts = _exchange_counts(need_counts, dev, group)
+    _trace("build_plan: exchange ids")
     # tell each owner which of its rows we need (global ids), learn what to send
     if world > 1:
         wanted = torch.empty(sum(give_counts), dtype=torch.int64, device=dev)
@@ -373,12 +398,15 @@ def partition_graph(edge_index: torch.Tensor, num_nodes: int, world: int, rank: 
     rank).  Collective over ``group`` (the halo lists are exchanged here).
     ``balance``: row blocks of equal size ("rows") or of equal modelled cost
     ("cost", :func:`row_bounds`)."""
+    _trace("partition_graph: row bounds")
     bounds = row_bounds(edge_index, num_nodes, world, balance)
+    _trace("partition_graph: masks")
     r0, r1 = bounds[rank], bounds[rank + 1]
     n = r1 - r0
     src, dst = edge_index[0], edge_index[1]
     ein = edge_index[:, (dst >= r0) & (dst < r1)]     # original order kept
     eout = edge_index[:, (src >= r0) & (src < r1)]
+    _trace("partition_graph: plans")
     remap_f, plan_f = _build_plan(ein[0], r0, r1, bounds, world, group)
     remap_b, plan_b = _build_plan(eout[1], r0, r1, bounds, world, group)
     n_buf_f = n + plan_f.num_recv
@@ -387,8 +415,10 @@ def partition_graph(edge_index: torch.Tensor, num_nodes: int, world: int, rank: 
     # source over buffer-position destinations; stable, so edge order is kept.
     fin = torch.stack([remap_f(ein[0]).long(), (ein[1] - r0).long()])
     fout = torch.stack([(eout[0] - r0).long(), remap_b(eout[1]).long()])
+    _trace("partition_graph: csr")
     rp, col, _, _ = backend.csr(fin, max(n_buf_f, 1), False)
     _, _, trp, tcol = backend.csr(fout, max(n_buf_b, 1), True)
+    _trace("partition_graph: split rows")
     fwd = SageGraph(n, int(ein.size(1)), rp[: n + 1], col, None, None)
     bwd = SageGraph(n, int(eout.size(1)), trp[: n + 1], tcol, None, None)
     return GraphPartition(rank, world, num_nodes, bounds, r0, r1, fwd, bwd, plan_f, plan_b,
@@ -1013,8 +1043,10 @@ def plan_partition(edge_index: torch.Tensor, num_nodes: int, world: int, rank: i
         if world == 1:
             strategy = "halo"
         else:
+            _trace("plan: estimate")
             info = estimate_strategies(edge_index, num_nodes, world, rank, feat, elem, group,
                                        link_bps)
+            _trace("plan: estimated")
             strategy = choose_strategy(info)
     info["strategy"] = strategy
     if strategy == "feature":
