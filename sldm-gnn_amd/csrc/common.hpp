@@ -28,8 +28,14 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(uint16_t, b);
 }
+// Two values, one v_cvt_pk_bf16_f32 (same rounding): written as a 2-vector
+// conversion because two scalar casts joined by shift / or lower to two
+// converts (each against a zero half) plus the shift and an SDWA or.
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  const f32x2_t v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
 // The value a float becomes once stored as T (bf16: rounded; fp32: itself).
@@ -310,7 +316,7 @@ int big_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int6
 bool stream_gemm_enabled();
 bool stream_dense_fwd_ok(int64_t k0, int64_t K, int64_t nc, const void* a0, int64_t lda0,
                          const void* a1, int64_t lda1, const void* w, const void* out,
-                         const void* xhat);
+                         const void* xhat, float slope);
 bool stream_rowscale_ok(int64_t k, int64_t nc, const void* a, int64_t lda, const void* b,
                         int64_t ldb, const void* out, int64_t ldo, int64_t scale_cols);
 int stream_dense_fwd(const void* a0, int64_t lda0, int64_t k0, const void* a1, int64_t lda1,

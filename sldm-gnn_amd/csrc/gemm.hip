@@ -995,7 +995,7 @@ extern "C" int sldm_sage_dense_fwd(int dtype, const void* a0, int64_t lda0, int6
                               negative_slope, drop_p, seed, row_off, out, xhat, rstd, stream);
   if (dtype == SLDM_BF16 && sldm::stream_gemm_enabled() &&
       sldm::stream_dense_fwd_ok(k0, k0 + k1, nc, a0, lda0, k1 ? a1 : a0, k1 ? lda1 : lda0, w,
-                                out, xhat))
+                                out, xhat, negative_slope))
     return sldm::stream_dense_fwd(a0, lda0, k0, a1, lda1, k1, w, num_rows, bias, gamma, beta,
                                   eps, negative_slope, drop_p, seed, row_off, out, xhat, rstd,
                                   stream);

@@ -17,9 +17,13 @@
 //    s_barrier per k-step;
 //  * a wave holds complete 256-column rows, so LayerNorm statistics reduce
 //    in-wave (two xor shuffles), with no LDS exchange and no block barrier in
-//    the epilogue; the LN outputs leave through a per-wave LDS staging tile as
-//    16-byte row-contiguous stores (row-per-lane 8-byte stores are
-//    store-issue-bound, MI355X_MICROARCH.md "epilogue store tail").
+//    the epilogue; the LN outputs leave as 16-byte stores, each lane's two
+//    4-column fragments of adjacent tiles paired by v_permlane16_swap (8
+//    columns contiguous per lane, 16 rows x 64 B per store instruction;
+//    row-per-lane 8-byte stores are store-issue-bound, MI355X_MICROARCH.md
+//    "epilogue store tail").  Same-box A/B at C4 (tools/ab_run1.sh): 4.74 ms
+//    against 4.79 ms through a per-wave LDS staging tile (SLDM_LN_STAGE=1,
+//    whole-row stores, 67 KB of LDS and an LDS round trip per output).
 //
 // vmcnt bookkeeping: per k-step every wave issues WIPW weight DMAs then 2
 // activation loads, so the slice consumed at step s is followed by exactly
@@ -36,7 +40,19 @@ typedef short s8v __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_vptr;
 
-constexpr int kThreads = 512;
+constexpr int kThreads = 512;   // ROWSCALE kernels: 8 waves, one workgroup per CU
+// LN forward launch shape: waves per workgroup (8: one 512-thread workgroup
+// per CU; 4: two 256-thread workgroups per CU, whose k-step barriers are
+// independent, so one workgroup's epilogue VALU can overlap the other's loads
+// -- measured slower, 5.38 vs 4.90 ms at C4: with 128-row tiles every CU
+// streams the 256 KB weight matrix from L2 twice as often) and whether its outputs leave through the LDS staging tile (1) or as
+// permlane16-paired 16-B stores (0; no staging LDS, required for 4 waves).
+#ifndef SLDM_LN_NW
+#define SLDM_LN_NW 8
+#endif
+#ifndef SLDM_LN_STAGE
+#define SLDM_LN_STAGE 0
+#endif
 constexpr int RW = 32;            // rows per wave
 constexpr int NTT = 16;           // 16-column MFMA tiles per wave (256 columns)
 constexpr int NSTW = 4;           // weight ring stages
@@ -47,7 +63,12 @@ constexpr int NSTW = 4;           // weight ring stages
 #ifndef SLDM_STREAM_DA
 #define SLDM_STREAM_DA 4
 #endif
-constexpr int DA = SLDM_STREAM_DA;
+// The LN forward's ring depth (its staging-free epilogue leaves the registers
+// for a deeper ring: more of the next tile's loads in flight under the
+// epilogue).
+#ifndef SLDM_LN_DA
+#define SLDM_LN_DA 4
+#endif
 // Diagnostic builds only (tools/ab_build.sh): 1 = the LN kernel storing z
 // without LayerNorm / activation / dropout (results wrong).
 #ifndef SLDM_STREAM_EXP
@@ -105,19 +126,22 @@ __device__ __forceinline__ void dma16(const void* sbase, uint32_t voff, uint32_t
                :: "v"(voff), "s"(sbase), "s"(lds_addr) : "memory", "m0");
 }
 
-template <int KSTEPS, int WN, int MODE>
+template <int KSTEPS, int WN, int MODE, int NW = 8, bool STAGE = true>
 constexpr size_t stream_lds_bytes() {
   return (size_t)NSTW * 256 * WN * 64 +
-         (MODE == ST_LN ? 3 * 256 * sizeof(float) + 8 * 16 * SROW : 0);
+         (MODE == ST_LN ? 3 * 256 * sizeof(float) + (STAGE ? NW * 16 * SROW : 0) : 0);
 }
 
-template <int KSTEPS, int WN, int MODE, bool SPLIT, bool HASDEG>
-__global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) {
-  constexpr int WR = 8 / WN;                 // row groups of 32 per tile
+template <int KSTEPS, int WN, int MODE, bool SPLIT, bool HASDEG, int NW = 8, bool STAGE = true,
+          int DA = SLDM_STREAM_DA>
+__global__ __launch_bounds__(NW * 64, 2) void gemm_stream_kernel(StreamArgs p) {
+  constexpr int NT_ = NW * 64;               // threads per workgroup
+  constexpr int WR = NW / WN;                // row groups of 32 per tile
   constexpr int BM = WR * RW;                // rows per tile
   constexpr int WCOLS = 256 * WN;            // weight rows staged per k-step
   constexpr int WSTAGE = WCOLS * 64;         // bytes per weight slice
-  constexpr int WIPW = WCOLS / 128;          // weight DMA instructions per wave per k-step
+  constexpr int WIPW = WCOLS / (NW * 16);    // weight DMA instructions per wave per k-step
+  static_assert(WCOLS % (NW * 16) == 0, "weight DMA rounds");
   constexpr int VM_BASE = 2 * WIPW + 6;
   // lower bound on epilogue vm ops per tile: LN 2 x 16 row stores (with
   // xhat, see loose_ok), ROWSCALE 2 x NTT/2 paired 16-B stores
@@ -142,7 +166,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
   if (tile >= p.ntiles) return;
 
   if constexpr (MODE == ST_LN) {
-    for (int i = tid; i < 256; i += kThreads) {
+    for (int i = tid; i < 256; i += NT_) {
       prm[i] = p.bias ? p.bias[i] : 0.f;
       prm[256 + i] = p.gamma[i];
       prm[512 + i] = p.beta[i];
@@ -156,7 +180,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
   // This lane's byte offset in W for DMA j = 0; DMA j adds the uniform
   // 128 W rows * ldb (on the scalar base): one VGPR for all WIPW DMAs.
   const uint32_t woff = (uint32_t)(((wave * 16 + drow) * (uint32_t)p.ldb + 8 * dchunk) * 2);
-  const uint32_t wstride = 128u * (uint32_t)p.ldb * 2u;
+  const uint32_t wstride = (uint32_t)(NW * 16) * (uint32_t)p.ldb * 2u;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_vptr)smem;   // LDS byte address
   auto issue_w = [&](int slot, int ks) {
     // bases laundered before the constant parts are added: otherwise every
@@ -167,7 +191,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
     wb += ks * 64;
     la += slot * WSTAGE + wave * 16 * 64;
 #pragma unroll
-    for (int j = 0; j < WIPW; ++j) dma16(wb + j * wstride, woff, la + j * 8 * 16 * 64);
+    for (int j = 0; j < WIPW; ++j) dma16(wb + j * wstride, woff, la + j * NW * 16 * 64);
   };
   // ---- activation fragments: lane (r16, q) <- row r16 (+16m), k 8q..8q+7 ----
   // Row pointers are formed once per tile; every k-step offset below is a
@@ -291,6 +315,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
     // ---- epilogue: acc[m][t][r] = C[row 16m + r16][col wc*256 + 16t + 4q + r]
     if constexpr (MODE == ST_LN) {
       char* stg = stage_base + wave * 16 * SROW;
+      (void)stg;
       const float inv_n = 1.0f / 256.f;
       const uint32_t dthr = sldm::dropout_threshold(p.drop_p);
       const int cq = 4 * q;
@@ -334,47 +359,93 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_stream_kernel(StreamArgs p) 
 #endif
         if (p.rstd && q == 0) p.rstd[row] = rs;
 
-        // two staging rounds through the wave's 16 x 512 B tile: xhat, then out
+        if constexpr (STAGE) {
+          // two staging rounds through the wave's 16 x 512 B tile: xhat, then out
 #pragma unroll
-        for (int pass = 0; pass < 2; ++pass) {
-          uint16_t* dst = pass == 0 ? p.xhat : p.out;
-          if (pass == 0 && !dst) continue;
+          for (int pass = 0; pass < 2; ++pass) {
+            uint16_t* dst = pass == 0 ? p.xhat : p.out;
+            if (pass == 0 && !dst) continue;
 #pragma unroll
-          for (int t = 0; t < NTT; ++t) {
-            const int c = 16 * t + cq;
-            float v[4];
-            if (pass == 0 || SLDM_STREAM_EXP == 1) {
+            for (int t = 0; t < NTT; ++t) {
+              const int c = 16 * t + cq;
+              float v[4];
+              if (pass == 0 || SLDM_STREAM_EXP == 1) {
 #pragma unroll
-              for (int r = 0; r < 4; ++r) v[r] = acc[m][t][r];
-            } else {
-              const f4v gg = *reinterpret_cast<const f4v*>(prm + 256 + c);
-              const f4v be = *reinterpret_cast<const f4v*>(prm + 512 + c);
-              bool keep[4] = {true, true, true, true};
-              if (p.drop_p > 0.f) {
-                sldm::dropout_keep2(rkey, (uint32_t)c, dthr, keep[0], keep[1]);
-                sldm::dropout_keep2(rkey, (uint32_t)c + 2, dthr, keep[2], keep[3]);
+                for (int r = 0; r < 4; ++r) v[r] = acc[m][t][r];
+              } else {
+                const f4v gg = *reinterpret_cast<const f4v*>(prm + 256 + c);
+                const f4v be = *reinterpret_cast<const f4v*>(prm + 512 + c);
+                bool keep[4] = {true, true, true, true};
+                if (p.drop_p > 0.f) {
+                  sldm::dropout_keep2(rkey, (uint32_t)c, dthr, keep[0], keep[1]);
+                  sldm::dropout_keep2(rkey, (uint32_t)c + 2, dthr, keep[2], keep[3]);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  const float y = acc[m][t][r] * gg[r] + be[r];
+                  const float a = fmaxf(y, y * p.slope);   // slope in [0, 1] (host-checked)
+                  v[r] = keep[r] ? a * p.drop_scale : 0.f;
+                }
               }
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const float y = acc[m][t][r] * gg[r] + be[r];
-                const float a = y > 0.f ? y : y * p.slope;
-                v[r] = keep[r] ? a * p.drop_scale : 0.f;
-              }
+              sldm::Vec<uint16_t, 4>::store(reinterpret_cast<uint16_t*>(stg + r16 * SROW + 2 * c),
+                                            v);
+              if (t & 1) __builtin_amdgcn_sched_barrier(0);   // bound hoisted prm reads
             }
-            sldm::Vec<uint16_t, 4>::store(reinterpret_cast<uint16_t*>(stg + r16 * SROW + 2 * c),
-                                          v);
-            if (t & 1) __builtin_amdgcn_sched_barrier(0);   // bound hoisted prm reads
-          }
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const int rr = 2 * i + (q >> 1);          // lane >> 5 (laundered ids)
-            const int cb = ((q & 1) * 16 + r16) * 16; // (lane & 31) * 16
-            const uint4 val = *reinterpret_cast<const uint4*>(stg + rr * SROW + cb);
-            const int64_t drow_ = min(row0 + rr, p.M - 1);
-            *reinterpret_cast<uint4*>(reinterpret_cast<char*>(dst + drow_ * p.ldo) + cb) = val;
+            for (int i = 0; i < 8; ++i) {
+              const int rr = 2 * i + (q >> 1);          // lane >> 5 (laundered ids)
+              const int cb = ((q & 1) * 16 + r16) * 16; // (lane & 31) * 16
+              const uint4 val = *reinterpret_cast<const uint4*>(stg + rr * SROW + cb);
+              const int64_t drow_ = min(row0 + rr, p.M - 1);
+              *reinterpret_cast<uint4*>(reinterpret_cast<char*>(dst + drow_ * p.ldo) + cb) = val;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           }
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        } else {
+          // permlane16-paired 16-B stores straight from the accumulators (the
+          // ROWSCALE epilogue's pattern below): a store instruction covers 16
+          // rows x 64 B, no staging LDS and no LDS round trip
+#pragma unroll
+          for (int pass = 0; pass < 2; ++pass) {
+            uint16_t* dst = pass == 0 ? p.xhat : p.out;
+            if (pass == 0 && !dst) continue;
+#pragma unroll
+            for (int t = 0; t < NTT; t += 2) {
+              uint32_t w[2][2];
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                const int c = 16 * (t + h) + cq;
+                float v[4];
+                if (pass == 0 || SLDM_STREAM_EXP == 1) {
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) v[r] = acc[m][t + h][r];
+                } else {
+                  const f4v gg = *reinterpret_cast<const f4v*>(prm + 256 + c);
+                  const f4v be = *reinterpret_cast<const f4v*>(prm + 512 + c);
+                  bool keep[4] = {true, true, true, true};
+                  if (p.drop_p > 0.f) {
+                    sldm::dropout_keep2(rkey, (uint32_t)c, dthr, keep[0], keep[1]);
+                    sldm::dropout_keep2(rkey, (uint32_t)c + 2, dthr, keep[2], keep[3]);
+                  }
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) {
+                    const float y = acc[m][t + h][r] * gg[r] + be[r];
+                    const float a = fmaxf(y, y * p.slope);   // slope in [0, 1] (host-checked)
+                    v[r] = keep[r] ? a * p.drop_scale : 0.f;
+                  }
+                }
+                w[h][0] = sldm::pack_bf16x2(v[0], v[1]);
+                w[h][1] = sldm::pack_bf16x2(v[2], v[3]);
+              }
+              auto s0 = __builtin_amdgcn_permlane16_swap(w[0][0], w[1][0], false, false);
+              auto s1 = __builtin_amdgcn_permlane16_swap(w[0][1], w[1][1], false, false);
+              const uint4 o = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+              const int cc = 16 * t + ((q & 1) ? 16 + 4 * (q - 1) : 4 * q);
+              *reinterpret_cast<uint4*>(dst + row * p.ldo + cc) = o;
+              __builtin_amdgcn_sched_barrier(0);   // bound hoisted prm reads
+            }
+          }
         }
       }
     } else {
@@ -448,15 +519,19 @@ int num_cus() {
 
 template <int KSTEPS, int WN, int MODE, bool SPLIT, bool HASDEG = false>
 int launch_stream(StreamArgs& p, hipStream_t stream) {
-  constexpr int BM = (8 / WN) * RW;
-  constexpr size_t lds = stream_lds_bytes<KSTEPS, WN, MODE>();
-  static_assert(lds <= 160 * 1024, "LDS budget");
+  constexpr int NW = MODE == ST_LN ? SLDM_LN_NW : 8;
+  constexpr bool STAGE = MODE == ST_LN ? SLDM_LN_STAGE != 0 : true;
+  constexpr int BM = (NW / WN) * RW;
+  constexpr size_t lds = stream_lds_bytes<KSTEPS, WN, MODE, NW, STAGE>();
+  constexpr int per_cu = 8 / NW;       // workgroups per CU (two waves per SIMD)
+  static_assert(lds * per_cu <= 160 * 1024, "LDS budget");
   p.ntiles = (p.M + BM - 1) / BM;
-  const int64_t grid = std::min<int64_t>(p.ntiles, num_cus());
-  auto kern = gemm_stream_kernel<KSTEPS, WN, MODE, SPLIT, HASDEG>;
+  const int64_t grid = std::min<int64_t>(p.ntiles, (int64_t)per_cu * num_cus());
+  constexpr int DAK = MODE == ST_LN ? SLDM_LN_DA : SLDM_STREAM_DA;
+  auto kern = gemm_stream_kernel<KSTEPS, WN, MODE, SPLIT, HASDEG, NW, STAGE, DAK>;
   SLDM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  kern<<<(unsigned)grid, kThreads, lds, stream>>>(p);
+  kern<<<(unsigned)grid, NW * 64, lds, stream>>>(p);
   SLDM_LAUNCH_CHECK("gemm_stream_kernel");
   return SLDM_OK;
 }
@@ -485,10 +560,14 @@ static bool stream_common_ok(int64_t k0, int64_t K, const void* a0, int64_t lda0
   return aligned16(a0) && (K == k0 || aligned16(a1)) && aligned16(b);
 }
 
+// The LN epilogue evaluates LeakyReLU as max(y, slope * y): equal to
+// (y > 0 ? y : slope * y), signed zeros and NaN included, for slope in [0, 1]
+// (ReLU and every leaky slope in use); other slopes take the tile kernels.
 bool stream_dense_fwd_ok(int64_t k0, int64_t K, int64_t nc, const void* a0, int64_t lda0,
                          const void* a1, int64_t lda1, const void* w, const void* out,
-                         const void* xhat) {
-  return nc == 256 && stream_common_ok(k0, K, a0, lda0, a1, lda1, w, K) && aligned16(out) &&
+                         const void* xhat, float slope) {
+  return nc == 256 && slope >= 0.f && slope <= 1.f &&
+         stream_common_ok(k0, K, a0, lda0, a1, lda1, w, K) && aligned16(out) &&
          (!xhat || aligned16(xhat));
 }
 

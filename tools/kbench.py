@@ -73,6 +73,12 @@ def main():
         add("gather_fwd", timeit(lambda: ops.gather_rows(x, gr.rowptr, gr.col, n, True), a.reps),
             e * (4 + f * s) + (n + 1) * 4 + n * f * s)
     fl = 2.0 * n * 2 * f * f
+    if want("dense1"):
+        # the default forward kernel only (library A/B)
+        for p_ in (0.25, 0.0):
+            ms = timeit(lambda: ops.sage_dense_fwd(agg, x, wcat, b, gam, bet, 1e-5, 0.1, p_, 7,
+                                                   True), a.reps)
+            add(f"dense_fwd p={p_} save=True", ms, 4 * n * f * s, fl)
     if want("dense"):
         for p_, save in [(0.25, True), (0.0, True), (0.0, False)]:
             ms = timeit(lambda: ops.sage_dense_fwd(agg, x, wcat, b, gam, bet, 1e-5, 0.1, p_, 7,
