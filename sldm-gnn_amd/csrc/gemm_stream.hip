@@ -63,12 +63,7 @@ constexpr int NSTW = 4;           // weight ring stages
 #ifndef SLDM_STREAM_DA
 #define SLDM_STREAM_DA 4
 #endif
-// The LN forward's ring depth (its staging-free epilogue leaves the registers
-// for a deeper ring: more of the next tile's loads in flight under the
-// epilogue).
-#ifndef SLDM_LN_DA
-#define SLDM_LN_DA 4
-#endif
+
 // Diagnostic builds only (tools/ab_build.sh): 1 = the LN kernel storing z
 // without LayerNorm / activation / dropout (results wrong).
 #ifndef SLDM_STREAM_EXP
@@ -527,8 +522,7 @@ int launch_stream(StreamArgs& p, hipStream_t stream) {
   static_assert(lds * per_cu <= 160 * 1024, "LDS budget");
   p.ntiles = (p.M + BM - 1) / BM;
   const int64_t grid = std::min<int64_t>(p.ntiles, (int64_t)per_cu * num_cus());
-  constexpr int DAK = MODE == ST_LN ? SLDM_LN_DA : SLDM_STREAM_DA;
-  auto kern = gemm_stream_kernel<KSTEPS, WN, MODE, SPLIT, HASDEG, NW, STAGE, DAK>;
+  auto kern = gemm_stream_kernel<KSTEPS, WN, MODE, SPLIT, HASDEG, NW, STAGE>;
   SLDM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   kern<<<(unsigned)grid, NW * 64, lds, stream>>>(p);

@@ -282,6 +282,34 @@ def test_post_fwd_bwd_vs_torch(f, slope):
     torch.testing.assert_close(db.cpu(), ber.grad, **tol)
 
 
+@pytest.mark.parametrize("dtype,f", [(torch.bfloat16, 256), (torch.float32, 128)])
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 1001, 70_001])
+@pytest.mark.parametrize("drop", [0.0, 0.25])
+def test_post_bwd_ring_equals_register_kernel(dtype, f, n, drop, monkeypatch):
+    """post.hip's LDS-ring LN backward (512-B rows: bf16 F = 256, fp32 F = 128)
+    against the register kernel (SLDM_POST_RING=0): dh bit for bit (same
+    per-element math), the column partials within summation-order tolerance;
+    odd row counts (the last pair holds one row), fewer pairs than waves and
+    several ring passes per wave included."""
+    from sldm_sage import ops
+    gen = torch.Generator(device=DEV).manual_seed(n + f)
+    xhat = torch.randn(n, f, generator=gen, device=DEV).to(dtype)
+    dout = torch.randn(n, f, generator=gen, device=DEV).to(dtype)
+    rstd = torch.rand(n, generator=gen, device=DEV) + 0.5
+    gam, bet = (torch.randn(f, generator=gen, device=DEV) for _ in range(2))
+
+    def run(ring):
+        monkeypatch.setenv("SLDM_POST_RING", "1" if ring else "0")
+        r = ops.post_bwd(dout, xhat, rstd, gam, bet, 0.1, drop, 99, dtype, row_offset=5)
+        torch.cuda.synchronize()
+        return r
+
+    got, ref = run(True), run(False)
+    assert torch.equal(got[0], ref[0])
+    for a, b in zip(got[1:], ref[1:]):
+        torch.testing.assert_close(a, b, atol=1e-4 * max(1.0, float(b.abs().max())), rtol=1e-5)
+
+
 @pytest.mark.parametrize("f", [16, 32, 96, 256, 10])
 def test_post_bwd_bf16_vs_torch(f):
     """bf16 storage of dout / xhat / dh, fp32 math, vs the same formula in fp32."""

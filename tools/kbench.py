@@ -115,6 +115,14 @@ def main():
         os.environ["SLDM_TN_DMA"] = "0"
         add("gemm_tn tiles", timeit(lambda: ops.gemm_tn(dh, agg, x), a.reps), 3 * n * f * s, fl)
         os.environ.pop("SLDM_TN_DMA")
+    if want("postring"):
+        out, xh, rs = ops.post_fwd(dh, None, gam, bet, 1e-5, 0.1, 0.0, 0, dt, True)
+        for ring in ("0", "1"):
+            os.environ["SLDM_POST_RING"] = ring
+            add(f"post_bwd p=0.25 ring={ring}",
+                timeit(lambda: ops.post_bwd(dh, xh, rs, gam, bet, 0.1, 0.25, 3, dt), a.reps),
+                3 * n * f * s)
+        os.environ.pop("SLDM_POST_RING")
     if want("post"):
         out, xh, rs = ops.post_fwd(dh, None, gam, bet, 1e-5, 0.1, 0.0, 0, dt, True)
         for p_, zo in [(0.0, None), (0.25, None), (0.25, out)]:
