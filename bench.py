@@ -429,7 +429,9 @@ def _parallelism(strategy, world):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20,
+                    help="timed steps (SURVEY.md §8d: >= 20 after 3 warm-ups, median reported "
+                         "as ms_per_step_median_rank0)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS) + sorted(SMALL_WORKLOADS),
                     help="a BASELINE graph config (c1-c5), or a real-workload line: vehicle / map "

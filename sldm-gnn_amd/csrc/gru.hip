@@ -51,8 +51,47 @@ __device__ __forceinline__ int aimg(int row, int k) {
   return ((q >> 2) * 64 + lane) * 4 + (q & 3);
 }
 
+
+// The x operand of both forward kernels (A: row c, k = 4q + g4), staged in
+// LDS TC steps at a time, double-buffered: chunk n + 2 is loaded into
+// registers when chunk n + 1 is written to LDS, TC steps before any step reads
+// it, so no step waits on a global load.  (Loaded one step ahead in registers,
+// the compiler drained vmcnt -- the previous step's output and gate stores
+// included -- at the top of every step: a store round trip per step.)  Both
+// forward kernels are held to 168 VGPRs (3 waves per SIMD: two 6-wave
+// workgroups per CU at H = 96) with the staging registers.
+constexpr int x_chunk_steps(int nw, int ki) {
+  return 4 * nw / ki >= 16 ? 16 : (4 * nw / ki >= 8 ? 8 : (4 * nw / ki >= 4 ? 4 : 2));
+}
 template <int NW, int KI>
-__global__ __launch_bounds__(64 * NW) void gru_fwd_kernel(
+struct XStage {
+  static constexpr int TC = x_chunk_steps(NW, KI);
+  static constexpr int CH = TC * KI * 64;                    // floats per chunk
+  static constexpr int PT = (CH + 64 * NW - 1) / (64 * NW);  // per thread
+  float r[PT];
+  __device__ __forceinline__ void load(const float* __restrict__ x, int64_t ldxn, int64_t ldxt,
+                                       int64_t N, int T, int I, int64_t r0, int t0) {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int e = (int)threadIdx.x + i * 64 * NW;
+      const int tt = e / (KI * 64), rem = e - tt * (KI * 64);
+      const int k = 4 * (rem >> 6) + ((rem & 63) >> 4);
+      const int t = t0 + tt;
+      const int64_t xr = min(r0 + (rem & 15), N - 1);
+      r[i] = (e < CH && k < I && t < T) ? x[xr * ldxn + (int64_t)t * ldxt + k] : 0.f;
+    }
+  }
+  __device__ __forceinline__ void store(float* buf) const {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int e = (int)threadIdx.x + i * 64 * NW;
+      if (e < CH) buf[e] = r[i];
+    }
+  }
+};
+
+template <int NW, int KI>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) void gru_fwd_kernel(
     const float* __restrict__ x, int64_t ldxn, int64_t ldxt, int64_t N, int T, int I,
     const float* __restrict__ w_ih, const float* __restrict__ w_hh,
     const float* __restrict__ b_ih, const float* __restrict__ b_hh,
@@ -93,21 +132,20 @@ __global__ __launch_bounds__(64 * NW) void gru_fwd_kernel(
     hp[r] = (h0 && row < N) ? h0[row * H + j] : 0.f;
     himg[0][aimg(4 * g4 + r, j)] = hp[r];
   }
-  // x operand (A: row c, k = 4q + g4), one step ahead
-  const int64_t xrow = min(r0 + c, N - 1);
-  auto load_x = [&](int t, float (&xa)[KI]) {
-#pragma unroll
-    for (int q = 0; q < KI; ++q) {
-      const int k = 4 * q + g4;
-      xa[q] = (k < I && t < T) ? x[xrow * ldxn + (int64_t)t * ldxt + k] : 0.f;
-    }
-  };
-  float xa[KI], xn[KI];
-  load_x(0, xa);
+  // x operand (A: row c, k = 4q + g4) from the LDS chunks (XStage)
+  using XS = XStage<NW, KI>;
+  __shared__ __attribute__((aligned(16))) float xs[2][XS::CH];
+  XS xst;
+  xst.load(x, ldxn, ldxt, N, T, I, r0, 0);
+  xst.store(xs[0]);
+  xst.load(x, ldxn, ldxt, N, T, I, r0, XS::TC);
   __syncthreads();
 
   for (int t = 0; t < T; ++t) {
-    load_x(t + 1, xn);
+    const int tt = t % XS::TC;
+    float xa[KI];
+#pragma unroll
+    for (int q = 0; q < KI; ++q) xa[q] = xs[(t / XS::TC) & 1][(tt * KI + q) * 64 + lane];
     const float* hi = himg[t & 1];
     f4v ar = {0.f, 0.f, 0.f, 0.f}, az = ar, an = ar, ahn = ar;
 #pragma unroll
@@ -147,8 +185,10 @@ __global__ __launch_bounds__(64 * NW) void gru_fwd_kernel(
                 ((((int64_t)t * gridDim.x + blockIdx.x) * NW + w) * 4) * 64 + lane;
       gp[0] = gr; gp[64] = gz; gp[128] = gn; gp[192] = gh;
     }
-#pragma unroll
-    for (int q = 0; q < KI; ++q) xa[q] = xn[q];
+    if (tt == XS::TC - 1 && t + 1 < T) {     // next chunk in, the one after loading
+      xst.store(xs[(t / XS::TC + 1) & 1]);
+      xst.load(x, ldxn, ldxt, N, T, I, r0, t + 1 + XS::TC);
+    }
     __syncthreads();
   }
   if (h_n) {
@@ -193,7 +233,7 @@ __device__ __forceinline__ int aimg32(int row, int k) {
 }
 
 template <int NW, int KI>
-__global__ __launch_bounds__(64 * NW) void gru_fwd_x3_kernel(
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) void gru_fwd_x3_kernel(
     const float* __restrict__ x, int64_t ldxn, int64_t ldxt, int64_t N, int T, int I,
     const float* __restrict__ w_ih, const float* __restrict__ w_hh,
     const float* __restrict__ b_ih, const float* __restrict__ b_hh,
@@ -246,20 +286,19 @@ __global__ __launch_bounds__(64 * NW) void gru_fwd_x3_kernel(
     hp[r] = (h0 && row < N) ? h0[row * H + j] : 0.f;
     himg[0][aimg32(4 * g4 + r, j)] = hp[r];
   }
-  const int64_t xrow = min(r0 + c, N - 1);
-  auto load_x = [&](int t, float (&xa)[KI]) {
-#pragma unroll
-    for (int q = 0; q < KI; ++q) {
-      const int k = 4 * q + g4;
-      xa[q] = (k < I && t < T) ? x[xrow * ldxn + (int64_t)t * ldxt + k] : 0.f;
-    }
-  };
-  float xa[KI], xn[KI];
-  load_x(0, xa);
+  using XS = XStage<NW, KI>;
+  __shared__ __attribute__((aligned(16))) float xs[2][XS::CH];
+  XS xst;
+  xst.load(x, ldxn, ldxt, N, T, I, r0, 0);
+  xst.store(xs[0]);
+  xst.load(x, ldxn, ldxt, N, T, I, r0, XS::TC);
   __syncthreads();
 
   for (int t = 0; t < T; ++t) {
-    load_x(t + 1, xn);
+    const int tt = t % XS::TC;
+    float xa[KI];
+#pragma unroll
+    for (int q = 0; q < KI; ++q) xa[q] = xs[(t / XS::TC) & 1][(tt * KI + q) * 64 + lane];
     const float* hi = himg[t & 1];
     f4v ar = {0.f, 0.f, 0.f, 0.f}, az = ar, an = ar, ahn = ar;
 #pragma unroll
@@ -305,8 +344,10 @@ __global__ __launch_bounds__(64 * NW) void gru_fwd_x3_kernel(
                 ((((int64_t)t * gridDim.x + blockIdx.x) * NW + w) * 4) * 64 + lane;
       gp[0] = gr; gp[64] = gz; gp[128] = gn; gp[192] = gh;
     }
-#pragma unroll
-    for (int q = 0; q < KI; ++q) xa[q] = xn[q];
+    if (tt == XS::TC - 1 && t + 1 < T) {     // next chunk in, the one after loading
+      xst.store(xs[(t / XS::TC + 1) & 1]);
+      xst.load(x, ldxn, ldxt, N, T, I, r0, t + 1 + XS::TC);
+    }
     __syncthreads();
   }
   if (h_n) {

@@ -85,7 +85,15 @@ __global__ __launch_bounds__(kBlock) void post_fwd_kernel(
 // One block per partial; grid-stride over row groups.  Column partials are
 // kept per thread (fixed columns), then combined across the block's row
 // groups in LDS and written as partials[blockIdx.x][3][feat].
-template <typename T, typename TD, int V, int NCH>
+// ZOUT (the saved-output branch source) is a template parameter: as a runtime
+// test its conditional load put a branch between the row loads, and the
+// compiler's vmcnt bookkeeping then drained every row's loads (vmcnt(0))
+// before issuing the next row's.  With both rows in flight the C4 time is the
+// same (3.26-3.30 ms; selects instead of the per-element branches: 3.46-3.50),
+// against 2.52 ms for torch.add over the same 2R:1W bytes: the loop's VALU
+// (LN math, dropout hash, exec-mask bookkeeping) is what holds it at
+// ~4.7 TB/s, not memory-level parallelism.
+template <typename T, typename TD, int V, int NCH, bool ZOUT>
 __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
     const T* __restrict__ dout, const T* __restrict__ xhat, const T* __restrict__ zout,
     const float* __restrict__ rstd,
@@ -135,7 +143,7 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
   for (int64_t it = 0; it < nrounds; ++it) {
     int64_t rr[RB];
     bool live[RB];
-    float go[RB][NCH][V], xh[RB][NCH][V], zo[RB][NCH][V], rsv[RB];
+    float go[RB][NCH][V], xh[RB][NCH][V], zo[RB][NCH][ZOUT ? V : 1], rsv[RB];
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
       const int64_t row = (it * RB + u) * stride + (int64_t)blockIdx.x * groups_per_block + group;
@@ -146,7 +154,7 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
       for (int c = 0; c < NCH; ++c) {
         sldm::Vec<T, V>::load(dout + rr[u] * (int64_t)feat + f0[c], go[u][c]);
         sldm::Vec<T, V>::load(xhat + rr[u] * (int64_t)feat + f0[c], xh[u][c]);
-        if (zout) sldm::Vec<T, V>::load(zout + rr[u] * (int64_t)feat + f0[c], zo[u][c]);
+        if constexpr (ZOUT) sldm::Vec<T, V>::load(zout + rr[u] * (int64_t)feat + f0[c], zo[u][c]);
       }
     }
 #pragma unroll
@@ -172,8 +180,9 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
           // y = fma(xhat, g, b), the forward epilogues' exact expression
           // (bit-equal y for fp32 storage; a bf16-rounded xhat can flip only
           // |y| within half an ulp of 0).
-          const bool pos = zout ? (keep ? zo[u][c][k] > 0.0f : true)
-                                : (__builtin_fmaf(xh[u][c][k], g, bt[c][k]) > 0.0f);
+          bool pos;
+          if constexpr (ZOUT) pos = keep ? zo[u][c][k] > 0.0f : true;
+          else pos = __builtin_fmaf(xh[u][c][k], g, bt[c][k]) > 0.0f;
           d = pos ? d : d * slope;
           if (!act[c] || !live[u]) { d = 0.0f; xh[u][c][k] = 0.0f; }
           dy[c][k] = d;
@@ -487,9 +496,16 @@ int post_bwd_nch(const RowGeom& g, const void* dout, const void* xhat, const voi
   }
 #define SLDM_PB_CASE(NC)                                                                       \
   case NC:                                                                                     \
-    post_bwd_kernel<T, TD, V, NC><<<np, kBlock, lds, stream>>>(                                \
-        reinterpret_cast<const T*>(dout), reinterpret_cast<const T*>(xhat), reinterpret_cast<const T*>(zout), rstd, nrows, feat, \
-        g.lpr_log2, gamma, beta, slope, p, scale, seed, row_off, reinterpret_cast<TD*>(dh), partials);  \
+    if (zout)                                                                                  \
+      post_bwd_kernel<T, TD, V, NC, true><<<np, kBlock, lds, stream>>>(                        \
+          reinterpret_cast<const T*>(dout), reinterpret_cast<const T*>(xhat),                  \
+          reinterpret_cast<const T*>(zout), rstd, nrows, feat, g.lpr_log2, gamma, beta, slope, \
+          p, scale, seed, row_off, reinterpret_cast<TD*>(dh), partials);                       \
+    else                                                                                       \
+      post_bwd_kernel<T, TD, V, NC, false><<<np, kBlock, lds, stream>>>(                       \
+          reinterpret_cast<const T*>(dout), reinterpret_cast<const T*>(xhat), nullptr, rstd,   \
+          nrows, feat, g.lpr_log2, gamma, beta, slope, p, scale, seed, row_off,                \
+          reinterpret_cast<TD*>(dh), partials);                                                \
     break;
   switch (g.nch) {
     SLDM_PB_CASE(1)

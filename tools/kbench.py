@@ -115,6 +115,16 @@ def main():
         os.environ["SLDM_TN_DMA"] = "0"
         add("gemm_tn tiles", timeit(lambda: ops.gemm_tn(dh, agg, x), a.reps), 3 * n * f * s, fl)
         os.environ.pop("SLDM_TN_DMA")
+    if want("mix"):
+        # the traffic mixes of the dense kernels through torch's elementwise
+        # kernels: the rate a plain streaming kernel reaches for them here
+        c = torch.empty_like(dh)
+        add("torch add 2R:1W [N,F]", timeit(lambda: torch.add(dh, x, out=c), a.reps), 3 * n * f * s)
+        add("torch copy 1R:1W [N,F]", timeit(lambda: c.copy_(dh), a.reps), 2 * n * f * s)
+        c2 = torch.empty(n, 2 * f, device=dev, dtype=dt)
+        add("torch cat 2R:2W [N,2F]", timeit(lambda: torch.cat([dh, x], 1, out=c2), a.reps),
+            4 * n * f * s)
+        del c, c2
     if want("postring"):
         out, xh, rs = ops.post_fwd(dh, None, gam, bet, 1e-5, 0.1, 0.0, 0, dt, True)
         for ring in ("0", "1"):
