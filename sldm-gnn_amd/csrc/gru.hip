@@ -226,6 +226,16 @@ __device__ __forceinline__ float fast_tanh(float v) { return 2.0f * fast_sigm(2.
 __device__ __forceinline__ f4v mfma32(s8b a, s8b b, f4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+typedef short s4b __attribute__((ext_vector_type(4)));   // 4 x bf16
+__device__ __forceinline__ f4v mfma16(s4b a, s4b b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ void split4(const float (&v)[4], s4b& hi, s4b& lo) {
+  uint2 h, l;
+  sldm::split_bf16x4(v, h, l);
+  hi = __builtin_bit_cast(s4b, h);
+  lo = __builtin_bit_cast(s4b, l);
+}
 // fp32 A-layout image of a [16 rows][KS*32] operand: element (row, k) of
 // k-step s = k >> 5 sits in lane row + 16 ((k & 31) >> 3), slot k & 7.
 __device__ __forceinline__ int aimg32(int row, int k) {
@@ -366,7 +376,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
 //   dGi  = [dar, daz, dan],  dGh = [dar, daz, dan r]
 //   dh_{t-1} += dGh W_hh                      (LDS image of dGh, W_hh frags)
 //   dW_hh += dGh^T h_{t-1}, dW_ih += dGi^T x_t, db += column sums
-template <int NW, int KI, bool X3>
+template <int NW, int KI, bool X3, bool DGI>
 __global__ __launch_bounds__(64 * NW) void gru_bwd_kernel(
     const float* __restrict__ x, int64_t ldxn, int64_t ldxt, int64_t N, int T, int I,
     const float* __restrict__ w_hh, const float* __restrict__ h0,
@@ -428,48 +438,56 @@ __global__ __launch_bounds__(64 * NW) void gru_bwd_kernel(
     live[r] = row < N;
     dh[r] = (dh_n && live[r]) ? dh_n[row * H + j] : 0.f;
   }
-  // x as the B operand of dW_ih: B[k <-> row 4 g4 + r][col i = c]
-  auto load_x = [&](int t, float (&xb)[4]) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t row = min(r0 + 4 * g4 + r, N - 1);
-      xb[r] = (c < I) ? x[row * ldxn + (int64_t)t * ldxt + c] : 0.f;
-    }
-  };
-
   // Step operands (saved gates, h_{t-1}, dout[t], x[t]) are loaded one step
-  // ahead: the loads of step t-1 are in flight while step t computes, instead
-  // of every step starting with a dependent global round trip.
+  // ahead, every load unconditional (clamped rows, sources and strides picked
+  // by scalar selects, values masked after the load) and every store of the loop unconditional
+  // (dgi has padded rows, DGI a template parameter): with a fixed op count per
+  // step the compiler's vmcnt waits release exactly the step they feed.  (With
+  // conditional loads and stores its bookkeeping fell back to waiting for the
+  // loads it had just issued: a global round trip per step.)
   struct StepIn {
     f4v gr, gz, gn, gh;
     float hp[4], go[4], xb[4];
   };
+  const int ci = c < I ? c : I - 1;
+  // source bases and strides chosen once (scalar selects), so the per-step
+  // addresses are plain arithmetic: h_{t-1} from out (t > 0) or h0 (t = 0;
+  // out again as a dummy when h0 is absent), dout likewise
+  const float* const h0p = h0 ? h0 : out;
+  const int64_t h0s = h0 ? H : ldon;
+  const float* const dp = dout ? dout : out;
+  const int64_t dsn = dout ? lddn : ldon, dst = dout ? lddt : 0;
   auto load_step = [&](int t, StepIn& in) {
+    const bool tp = t > 0;
+    const float* const hb = tp ? out : h0p;   // (t = 0 without h0: a dummy row of out)
+    const int64_t hsn = tp ? ldon : h0s, hst = tp ? (int64_t)(t - 1) * ldot : 0;
     const f4v* gp = reinterpret_cast<const f4v*>(gates) +
                     ((((int64_t)t * gridDim.x + blockIdx.x) * NW + w) * 4) * 64 + lane;
     in.gr = gp[0]; in.gz = gp[64]; in.gn = gp[128]; in.gh = gp[192];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t row = min(r0 + 4 * g4 + r, N - 1);
-      in.hp[r] = t > 0 ? out[row * ldon + (int64_t)(t - 1) * ldot + j]
-                       : (h0 ? h0[row * H + j] : 0.f);
-      in.go[r] = (dout && live[r]) ? dout[row * lddn + (int64_t)t * lddt + j] : 0.f;
+      // raw values: the masks are applied where the step consumes them (a
+      // select here lets the compiler skip -- i.e. branch around -- the load)
+      in.hp[r] = hb[row * hsn + hst + j];
+      in.go[r] = dp[row * dsn + (int64_t)t * dst + j];
+      // x as the B operand of dW_ih: B[k <-> row 4 g4 + r][col i = c]
+      in.xb[r] = x[row * ldxn + (int64_t)t * ldxt + ci];
     }
-    load_x(t, in.xb);
   };
   StepIn nxt;
   load_step(T - 1, nxt);
   for (int t = T - 1; t >= 0; --t) {
     const int b = t & 1;
     const StepIn cur = nxt;
-    if (t > 0) load_step(t - 1, nxt);
+    load_step(t > 0 ? t - 1 : 0, nxt);   // at step 0: a harmless re-load
     const f4v gr = cur.gr, gz = cur.gz, gn = cur.gn, gh = cur.gh;
     float hp[4], xb[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      hp[r] = cur.hp[r];
-      xb[r] = cur.xb[r];
-      dh[r] += cur.go[r];
+      hp[r] = (t > 0 || h0) ? cur.hp[r] : 0.f;
+      xb[r] = c < I ? cur.xb[r] : 0.f;
+      dh[r] += (dout && live[r]) ? cur.go[r] : 0.f;
     }
     f4v dar, daz, dan, dghn;
 #pragma unroll
@@ -500,11 +518,11 @@ __global__ __launch_bounds__(64 * NW) void gru_bwd_kernel(
       }
     }
     *reinterpret_cast<f4v*>(&pimg[b][(w * 64 + lane) * 4]) = f4v{hp[0], hp[1], hp[2], hp[3]};
-    if (dgi) {                              // dx needs dGi: [N, T, 3H] in (row, t) order
+    if constexpr (DGI) {                    // dx needs dGi: [rows, T, 3H] in (row, t) order
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+        // rows past N land in the workspace's padding rows (unconditional)
         const int64_t row = r0 + 4 * g4 + r;
-        if (!live[r]) continue;
         float* o = dgi + (row * T + t) * (int64_t)(3 * H);
         o[j] = dar[r];
         o[H + j] = daz[r];
@@ -545,21 +563,61 @@ __global__ __launch_bounds__(64 * NW) void gru_bwd_kernel(
 
     // dW_hh[g H + 16 w + c'][16 kt + c''] += sum_rows dGh h_{t-1}: A = this
     // lane's dGh registers (k-step r <-> row 4 g4 + r), B = h_{t-1} tile kt
+    if constexpr (X3) {
+      // The 16 rows of a step are exactly the K = 16 of one
+      // v_mfma_f32_16x16x16_bf16 (lane (c, g4) supplies k = 4 g4 + r, the
+      // same rows the four fp32 16x16x4 steps take): split form, three bf16
+      // MFMAs per tile instead of four fp32 ones -- the weight-gradient
+      // accumulation was the longest MFMA chain of a step (6 x 3 tiles).
+      const float va[3][4] = {{dar[0], dar[1], dar[2], dar[3]},
+                              {daz[0], daz[1], daz[2], daz[3]},
+                              {dghn[0], dghn[1], dghn[2], dghn[3]}};
+      s4b ahi[3], alo[3];
 #pragma unroll
-    for (int kt = 0; kt < NW; ++kt) {
-      const f4v hb = *reinterpret_cast<const f4v*>(&pimg[b][(kt * 64 + lane) * 4]);
+      for (int g = 0; g < 3; ++g) split4(va[g], ahi[g], alo[g]);
+#pragma unroll
+      for (int kt = 0; kt < NW; ++kt) {
+        const f4v hb = *reinterpret_cast<const f4v*>(&pimg[b][(kt * 64 + lane) * 4]);
+        const float vb[4] = {hb[0], hb[1], hb[2], hb[3]};
+        s4b bhi, blo;
+        split4(vb, bhi, blo);
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          dwh[g][kt] = mfma16(alo[g], bhi, dwh[g][kt]);
+          dwh[g][kt] = mfma16(ahi[g], blo, dwh[g][kt]);
+          dwh[g][kt] = mfma16(ahi[g], bhi, dwh[g][kt]);
+        }
+      }
+      const float vx[4] = {xb[0], xb[1], xb[2], xb[3]};
+      const float vn[4] = {dan[0], dan[1], dan[2], dan[3]};
+      s4b xhi, xlo, nhi, nlo;
+      split4(vx, xhi, xlo);
+      split4(vn, nhi, nlo);
+      const s4b* aih[3] = {&ahi[0], &ahi[1], &nhi};
+      const s4b* ail[3] = {&alo[0], &alo[1], &nlo};
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        dwi[g] = mfma16(*ail[g], xhi, dwi[g]);
+        dwi[g] = mfma16(*aih[g], xlo, dwi[g]);
+        dwi[g] = mfma16(*aih[g], xhi, dwi[g]);
+      }
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < NW; ++kt) {
+        const f4v hb = *reinterpret_cast<const f4v*>(&pimg[b][(kt * 64 + lane) * 4]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dwh[0][kt] = mfma4(dar[r], hb[r], dwh[0][kt]);
+          dwh[1][kt] = mfma4(daz[r], hb[r], dwh[1][kt]);
+          dwh[2][kt] = mfma4(dghn[r], hb[r], dwh[2][kt]);
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        dwh[0][kt] = mfma4(dar[r], hb[r], dwh[0][kt]);
-        dwh[1][kt] = mfma4(daz[r], hb[r], dwh[1][kt]);
-        dwh[2][kt] = mfma4(dghn[r], hb[r], dwh[2][kt]);
+        dwi[0] = mfma4(dar[r], xb[r], dwi[0]);
+        dwi[1] = mfma4(daz[r], xb[r], dwi[1]);
+        dwi[2] = mfma4(dan[r], xb[r], dwi[2]);
       }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      dwi[0] = mfma4(dar[r], xb[r], dwi[0]);
-      dwi[1] = mfma4(daz[r], xb[r], dwi[1]);
-      dwi[2] = mfma4(dan[r], xb[r], dwi[2]);
     }
   }
   if (dh0) {
@@ -692,9 +750,10 @@ int launch_bwd(dim3 grid, hipStream_t st, const float* x, int64_t ldxn, int64_t 
   static_assert(lds <= 160 * 1024, "GRU backward LDS budget");
   // the split form needs the 3H gate columns in whole 32-deep k-steps
   // (H = 32, 64, 96); other sizes run the fp32 MFMA recurrence
-  auto kern = gru_bwd_kernel<NW, 1, false>;
+  auto kern = dgi ? gru_bwd_kernel<NW, 1, false, true> : gru_bwd_kernel<NW, 1, false, false>;
   if constexpr ((3 * H) % 32 == 0) {
-    if (gru_bf16x3_enabled()) kern = gru_bwd_kernel<NW, 1, true>;
+    if (gru_bf16x3_enabled())
+      kern = dgi ? gru_bwd_kernel<NW, 1, true, true> : gru_bwd_kernel<NW, 1, true, false>;
   }
   SLDM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -746,7 +805,8 @@ extern "C" size_t sldm_gru_bwd_workspace_bytes(int64_t N, int64_t T, int64_t I, 
   if (N <= 0 || T <= 0 || H <= 0) return 16;
   const int64_t tiles = (N + 15) / 16;
   size_t b = (size_t)tiles * (3 * H * H + 3 * H * 16 + 4 * H) * sizeof(float);
-  if (need_dx) b += (size_t)N * T * 3 * H * sizeof(float);
+  // dGi rows padded to whole 16-row tiles (the backward stores them unconditionally)
+  if (need_dx) b += (size_t)tiles * 16 * T * 3 * H * sizeof(float);
   return b;
 }
 
