@@ -17,11 +17,15 @@
 //      gathers sum in the same order bit for bit) and replace them by the
 //      batch-global neighbour ids.
 // Integer work on a few MB per batch: launch- and latency-bound, not HBM-bound.
-// When a launch's graphs fit (LDS: 2 counters per node + 2 ids per edge), the
-// edge ids are scattered and sorted in LDS and leave in one coalesced pass
-// (the vehicle packs: ~250 nodes, ~5k edges); otherwise the sort runs on the
-// global col / t_col slices.  The global variant was 225 us per 32-pack batch:
-// each row's insertion sort is a chain of dependent global round trips.
+// Three variants by LDS fit (per launch, from its largest graph): (2) the
+// graph's (src, dst) pairs staged in LDS as int32 local ids while step 1
+// reads them, edge ids scattered and sorted in LDS, neighbour ids written in
+// one coalesced pass from LDS -- the vehicle packs (~250 nodes, ~5k edges);
+// (1) the same without the staged pairs (steps 3 and 5 re-read edge_index);
+// (0) rows sorted in the global col / t_col slices.  Step 1 keeps kBatch
+// edges' loads in flight per thread.  r2: the global variant took 225 us per
+// 32-pack batch (each row's insertion sort a chain of dependent global round
+// trips), variant 1 with one load per edge per iteration 125 us.
 constexpr size_t kLdsBudget = 160 * 1024;
 #include "common.hpp"
 
@@ -69,7 +73,15 @@ __device__ void block_exclusive_scan(int32_t* cnt, int n, int32_t* part) {
   __syncthreads();
 }
 
-template <bool IN_LDS>
+// MODE 0: CSR rows sorted in global memory; 1: edge ids scattered and sorted
+// in LDS; 2: as 1 with the graph's (src, dst) pairs also staged in LDS as
+// int32 local ids during step 1, so steps 3 and 5 never touch global memory.
+// Step 1 issues kBatch edges' loads per thread before using any of them (the
+// out_ei stores may alias ei as far as the compiler knows, so a plain loop
+// was one dependent global round trip per edge: ~20 per thread per phase).
+constexpr int kBatch = 8;
+
+template <int MODE>
 __global__ __launch_bounds__(kThreads) void batch_graphs_kernel(BatchArgs p) {
   extern __shared__ int32_t lds[];
   const int gl = blockIdx.x;
@@ -80,6 +92,10 @@ __global__ __launch_bounds__(kThreads) void batch_graphs_kernel(BatchArgs p) {
   int32_t* cd = lds;                 // in-degree counters, then cursors
   int32_t* cs = lds + N;             // out-degree counters, then cursors
   int32_t* part = lds + 2 * N;       // scan scratch [kThreads]
+  int32_t* ecol = part + kThreads;   // MODE >= 1: [E] dst-CSR local edge ids
+  int32_t* tcol = ecol + E;          // MODE >= 1: [E] src-CSR local edge ids
+  int32_t* sl = tcol + E;            // MODE 2: [E] local source ids (-1: invalid edge)
+  int32_t* dl = sl + E;              // MODE 2: [E] local destination ids
   const int t = threadIdx.x;
 
   for (int i = t; i < 2 * N; i += kThreads) lds[i] = 0;
@@ -94,18 +110,34 @@ __global__ __launch_bounds__(kThreads) void batch_graphs_kernel(BatchArgs p) {
   }
   __syncthreads();
 
-  // 1. copy + offset, validate, count
+  // 1. copy + offset, validate, count (kBatch edges' loads in flight per thread)
   bool bad = false;
-  for (int64_t e = t; e < E; e += kThreads) {
-    const int64_t s = ei[e], d = ei[st + e];
-    const bool ok = (s >= 0) & (s < N) & (d >= 0) & (d < N);
-    p.out_ei[eoff + e] = s + noff;
-    p.out_ei[p.out_ld + eoff + e] = d + noff;
-    if (ok) {
-      atomicAdd(&cd[d], 1);
-      atomicAdd(&cs[s], 1);
+  for (int64_t e0 = t; e0 < E; e0 += (int64_t)kThreads * kBatch) {
+    int64_t s[kBatch], d[kBatch];
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u) {
+      const int64_t e = min(e0 + (int64_t)u * kThreads, E - 1);   // clamped: loads unconditional
+      s[u] = ei[e];
+      d[u] = ei[st + e];
     }
-    bad |= !ok;
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u) {
+      const int64_t e = e0 + (int64_t)u * kThreads;
+      if (e < E) {
+        const bool ok = (s[u] >= 0) & (s[u] < N) & (d[u] >= 0) & (d[u] < N);
+        p.out_ei[eoff + e] = s[u] + noff;
+        p.out_ei[p.out_ld + eoff + e] = d[u] + noff;
+        if (ok) {
+          atomicAdd(&cd[d[u]], 1);
+          atomicAdd(&cs[s[u]], 1);
+        }
+        if constexpr (MODE == 2) {
+          sl[e] = ok ? (int32_t)s[u] : -1;
+          dl[e] = (int32_t)d[u];
+        }
+        bad |= !ok;
+      }
+    }
   }
   if (bad) atomicOr(p.bad, 1);
   __syncthreads();
@@ -119,16 +151,34 @@ __global__ __launch_bounds__(kThreads) void batch_graphs_kernel(BatchArgs p) {
   }
   __syncthreads();
 
-  if constexpr (IN_LDS) {
+  if constexpr (MODE >= 1) {
     // 3'. scatter local edge ids into LDS, 4'. sort each row there, then the
-    // neighbour ids leave in one coalesced pass (independent loads of ei)
-    int32_t* ecol = part + kThreads;          // [E] dst-CSR local edge ids
-    int32_t* tcol = ecol + E;                 // [E] src-CSR local edge ids
-    for (int64_t e = t; e < E; e += kThreads) {
-      const int64_t s = ei[e], d = ei[st + e];
-      if ((s >= 0) & (s < N) & (d >= 0) & (d < N)) {
-        ecol[atomicAdd(&cd[d], 1)] = (int32_t)e;
-        if (p.t_col) tcol[atomicAdd(&cs[s], 1)] = (int32_t)e;
+    // neighbour ids leave in one coalesced pass
+    if constexpr (MODE == 2) {
+      for (int64_t e = t; e < E; e += kThreads) {
+        const int32_t s = sl[e];
+        if (s >= 0) {
+          ecol[atomicAdd(&cd[dl[e]], 1)] = (int32_t)e;
+          if (p.t_col) tcol[atomicAdd(&cs[s], 1)] = (int32_t)e;
+        }
+      }
+    } else {
+      for (int64_t e0 = t; e0 < E; e0 += (int64_t)kThreads * kBatch) {
+        int64_t s[kBatch], d[kBatch];
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) {
+          const int64_t e = min(e0 + (int64_t)u * kThreads, E - 1);
+          s[u] = ei[e];
+          d[u] = ei[st + e];
+        }
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) {
+          const int64_t e = e0 + (int64_t)u * kThreads;
+          if (e < E && (s[u] >= 0) & (s[u] < N) & (d[u] >= 0) & (d[u] < N)) {
+            ecol[atomicAdd(&cd[d[u]], 1)] = (int32_t)e;
+            if (p.t_col) tcol[atomicAdd(&cs[s[u]], 1)] = (int32_t)e;
+          }
+        }
       }
     }
     __syncthreads();
@@ -151,11 +201,17 @@ __global__ __launch_bounds__(kThreads) void batch_graphs_kernel(BatchArgs p) {
     __syncthreads();
     // rows past a bad id are short; those batches raise on the host anyway
     const int64_t Ev = N > 0 ? cd[N - 1] : 0;
-    for (int64_t k = t; k < Ev; k += kThreads)
-      p.col[eoff + k] = (int32_t)(ei[ecol[k]] + noff);
-    if (p.t_col)
+    if constexpr (MODE == 2) {
+      for (int64_t k = t; k < Ev; k += kThreads) p.col[eoff + k] = sl[ecol[k]] + (int32_t)noff;
+      if (p.t_col)
+        for (int64_t k = t; k < Ev; k += kThreads) p.t_col[eoff + k] = dl[tcol[k]] + (int32_t)noff;
+    } else {
       for (int64_t k = t; k < Ev; k += kThreads)
-        p.t_col[eoff + k] = (int32_t)(ei[st + tcol[k]] + noff);
+        p.col[eoff + k] = (int32_t)(ei[ecol[k]] + noff);
+      if (p.t_col)
+        for (int64_t k = t; k < Ev; k += kThreads)
+          p.t_col[eoff + k] = (int32_t)(ei[st + tcol[k]] + noff);
+    }
     return;
   }
 
@@ -227,10 +283,12 @@ extern "C" int sldm_batch_graphs(int64_t num_graphs, const int64_t* const* edge_
   hipStream_t stream = sldm::as_stream(stream_);
   SLDM_HIP_CHECK(hipMemsetAsync(bad_index_flag, 0, sizeof(int32_t), stream));
   const size_t lds_cnt = (size_t)(2 * max_n + kThreads) * sizeof(int32_t);
-  const size_t lds_all = lds_cnt + (size_t)2 * max_e * sizeof(int32_t);
-  const bool in_lds = lds_all <= kLdsBudget;
-  const size_t lds = in_lds ? lds_all : lds_cnt;
-  auto kern = in_lds ? batch_graphs_kernel<true> : batch_graphs_kernel<false>;
+  const size_t lds_ids = lds_cnt + (size_t)2 * max_e * sizeof(int32_t);
+  const size_t lds_stg = lds_cnt + (size_t)4 * max_e * sizeof(int32_t);
+  const int mode = lds_stg <= kLdsBudget ? 2 : (lds_ids <= kLdsBudget ? 1 : 0);
+  const size_t lds = mode == 2 ? lds_stg : (mode == 1 ? lds_ids : lds_cnt);
+  auto kern = mode == 2 ? batch_graphs_kernel<2>
+                        : (mode == 1 ? batch_graphs_kernel<1> : batch_graphs_kernel<0>);
   SLDM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int64_t noff = 0, eoff = 0;

@@ -958,7 +958,16 @@ TnPlan tn_plan(int64_t rows, int64_t mo, int64_t nn) {
   // 768 measured best at C4 (10M rows: 4.63 -> 3.84 ms vs 512); short node
   // dimensions keep 512 (C2: the extra slabs cost more than they hide)
   int64_t splits = (target ? target : (rows >= 2000000 ? 768 : 512)) / tiles;
-  const int64_t max_splits = (rows + 8 * TN_BK - 1) / (8 * TN_BK);  // >= 8 k-steps each
+  // >= 8 k-steps per split on long node dimensions; short ones (the vehicle
+  // batches' ~8k rows: 31 splits = 48 blocks of 11 k-steps, 40 us of mostly
+  // idle CUs) take more, shorter splits; SLDM_TN_MINK overrides (A/B runs)
+  static const int64_t mink_env = [] {
+    const char* e = getenv("SLDM_TN_MINK");
+    const long v = e ? atol(e) : 0;
+    return (int64_t)(v > 0 ? v : 0);
+  }();
+  const int64_t mink = mink_env ? mink_env : (rows >= 65536 ? 8 : 3);
+  const int64_t max_splits = (rows + mink * TN_BK - 1) / (mink * TN_BK);
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   if (splits >= 8) splits = (splits / 8) * 8;

@@ -142,6 +142,9 @@ def _device_graphs(spec, seed=0):
     [(250, 6000, ""), (300, 9000, ""), (0, 0, ""), (1, 3, ""), (40, 0, ""), (220, 5000, "strided")],
     [(n, 8 * n, "") for n in range(1, 60)],                 # > 48 graphs: two launches
     [(2000, 3000, "star"), (5, 40, ""), (16384, 20000, "")],  # high degree, max nodes
+    # LDS variants of batch.hip by the launch's largest graph: edge pairs staged
+    # (above: <= ~9.9k edges at 250 nodes), edge ids only (here), global (above)
+    [(3000, 12000, ""), (100, 500, "strided"), (7, 0, "")],
 ])
 def test_device_collate_fused_batch_matches_pyg_and_csr_build(spec):
     """The fused GPU batching kernel (batch.hip): edge_index / batch / ptr as
