@@ -5,7 +5,7 @@
 // (PyG __inc__), the `batch` and `ptr` vectors -- fused with the batch's CSR
 // pair, so a collated batch reaches the SageBlock with its CSR already built.
 //
-// One 256-thread workgroup per graph (the graphs' edges never cross graphs,
+// One 1024-thread workgroup per graph (the graphs' edges never cross graphs,
 // so each graph's CSR rows are a contiguous slice of the batch CSR):
 //   1. copy + offset edge_index, write batch / ptr, validate ids, count in-
 //      and out-degrees into LDS counters (ds atomics);
@@ -19,8 +19,9 @@
 // Integer work on a few MB per batch: launch- and latency-bound, not HBM-bound.
 // Three variants by LDS fit (per launch, from its largest graph): (2) the
 // graph's (src, dst) pairs staged in LDS as int32 local ids while step 1
-// reads them, edge ids scattered and sorted in LDS, neighbour ids written in
-// one coalesced pass from LDS -- the vehicle packs (~250 nodes, ~5k edges);
+// reads them, edge ids scattered in LDS, and each slot's neighbour id written
+// straight to its row position by rank (no per-row sort) -- the vehicle packs
+// (~250 nodes, ~5k edges);
 // (1) the same without the staged pairs (steps 3 and 5 re-read edge_index);
 // (0) rows sorted in the global col / t_col slices.  Step 1 keeps kBatch
 // edges' loads in flight per thread.  r2: the global variant took 225 us per
@@ -31,7 +32,7 @@ constexpr size_t kLdsBudget = 160 * 1024;
 
 namespace {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 1024;       // 16 waves: one workgroup per CU (LDS), latency hidden by waves
 constexpr int kMaxGraphs = 48;          // per launch (kernel-argument budget)
 constexpr int kMaxNodes = 16384;        // per graph: 2 x 64 KB LDS counters
 
@@ -57,7 +58,7 @@ __device__ void block_exclusive_scan(int32_t* cnt, int n, int32_t* part) {
   for (int i = b; i < e; ++i) s += cnt[i];
   part[t] = s;
   __syncthreads();
-  // Hillis-Steele over the 256 segment sums
+  // Hillis-Steele over the kThreads segment sums
   for (int off = 1; off < kThreads; off <<= 1) {
     const int32_t v = t >= off ? part[t - off] : 0;
     __syncthreads();
@@ -182,6 +183,34 @@ __global__ __launch_bounds__(kThreads) void batch_graphs_kernel(BatchArgs p) {
       }
     }
     __syncthreads();
+    // rows past a bad id are short; those batches raise on the host anyway
+    const int64_t Ev = N > 0 ? cd[N - 1] : 0;
+    if constexpr (MODE == 2) {
+      // 4''. no sort: each slot's edge goes to its row position by rank, the
+      // number of the row's edge ids below its own (all rows in parallel, one
+      // independent LDS read per comparison).  The serial per-row insertion
+      // sort was the kernel's critical path: the LDS atomics of one
+      // instruction hand out a row's slots in an order that can be the
+      // reverse of the lanes' edge order, and a reversed row of d entries is
+      // d^2 / 2 dependent LDS round trips on one thread.
+      for (int dir = 0; dir < (p.t_col ? 2 : 1); ++dir) {
+        const int32_t* r = dir == 0 ? ecol : tcol;
+        const int32_t* cur = dir == 0 ? cd : cs;
+        const int32_t* key = dir == 0 ? dl : sl;     // the edge's row
+        const int32_t* nbr = dir == 0 ? sl : dl;     // its neighbour
+        int32_t* outc = (dir == 0 ? p.col : p.t_col) + eoff;
+        for (int64_t k = t; k < Ev; k += kThreads) {
+          const int32_t e = r[k];
+          const int32_t row = key[e];
+          const int32_t b = row == 0 ? 0 : cur[row - 1], en = cur[row];
+          int32_t rank = 0;
+#pragma unroll 8
+          for (int32_t j = b; j < en; ++j) rank += r[j] < e;
+          outc[b + rank] = nbr[e] + (int32_t)noff;
+        }
+      }
+      return;
+    }
     for (int dir = 0; dir < (p.t_col ? 2 : 1); ++dir) {
       int32_t* r = dir == 0 ? ecol : tcol;
       const int32_t* cur = dir == 0 ? cd : cs;
@@ -199,19 +228,11 @@ __global__ __launch_bounds__(kThreads) void batch_graphs_kernel(BatchArgs p) {
       }
     }
     __syncthreads();
-    // rows past a bad id are short; those batches raise on the host anyway
-    const int64_t Ev = N > 0 ? cd[N - 1] : 0;
-    if constexpr (MODE == 2) {
-      for (int64_t k = t; k < Ev; k += kThreads) p.col[eoff + k] = sl[ecol[k]] + (int32_t)noff;
-      if (p.t_col)
-        for (int64_t k = t; k < Ev; k += kThreads) p.t_col[eoff + k] = dl[tcol[k]] + (int32_t)noff;
-    } else {
+    for (int64_t k = t; k < Ev; k += kThreads)
+      p.col[eoff + k] = (int32_t)(ei[ecol[k]] + noff);
+    if (p.t_col)
       for (int64_t k = t; k < Ev; k += kThreads)
-        p.col[eoff + k] = (int32_t)(ei[ecol[k]] + noff);
-      if (p.t_col)
-        for (int64_t k = t; k < Ev; k += kThreads)
-          p.t_col[eoff + k] = (int32_t)(ei[st + tcol[k]] + noff);
-    }
+        p.t_col[eoff + k] = (int32_t)(ei[st + tcol[k]] + noff);
     return;
   }
 
