@@ -184,6 +184,15 @@ int sldm_gemm_tn(int dtype, const void* a, int64_t lda, int64_t mo,
                  const void* b1, int64_t ldb1, int64_t n1,
                  int64_t num_rows, float* out, void* workspace, size_t workspace_bytes,
                  void* stream);
+/* The same product written as its two column blocks, out0[mo, n0] (= dW_l)
+ * and out1[mo, n1] (= dW_r), each contiguous: the parameter gradients of
+ * lin_l / lin_r (sageblock.py:8 SAGEConv, A8) without two slicing copies.
+ * n0, n1 > 0; same workspace as sldm_gemm_tn; bit-identical values. */
+int sldm_gemm_tn_split(int dtype, const void* a, int64_t lda, int64_t mo,
+                       const void* b0, int64_t ldb0, int64_t n0,
+                       const void* b1, int64_t ldb1, int64_t n1,
+                       int64_t num_rows, float* out0, float* out1, void* workspace,
+                       size_t workspace_bytes, void* stream);
 
 /* Fused layer boundary of the backward: the transpose gather of layer l
  * (dx_l = addend + sum over out-edges of g, rows in row_order or 0..N-1)

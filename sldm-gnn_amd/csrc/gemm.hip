@@ -932,9 +932,13 @@ __global__ __launch_bounds__(kBlock) void gemm_tn_kernel(TnArgs<T> p) {
     }
 }
 
+// out1 != nullptr: element (row, col) of the [mo, nn] result goes to out
+// [mo, n0] for col < n0 and to out1 [mo, nn - n0] otherwise (dW_l, dW_r).
 __global__ __launch_bounds__(kBlock) void slab_reduce_kernel(const float* __restrict__ slab,
                                                              int splits, int64_t n,
-                                                             float* __restrict__ out) {
+                                                             float* __restrict__ out,
+                                                             float* __restrict__ out1, int64_t n0,
+                                                             int64_t nn) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   // Sum over the splits in split order (deterministic, fixed bits); the loads
@@ -951,7 +955,13 @@ __global__ __launch_bounds__(kBlock) void slab_reduce_kernel(const float* __rest
     for (int u = 0; u < U; ++u) s += v[u];
   }
   for (; k < splits; ++k) s += slab[(int64_t)k * n + i];
-  out[i] = s;
+  if (out1) {
+    const int64_t row = i / nn, col = i - row * nn;
+    if (col < n0) out[row * n0 + col] = s;
+    else out1[row * (nn - n0) + (col - n0)] = s;
+  } else {
+    out[i] = s;
+  }
 }
 
 struct TnPlan {
@@ -1110,10 +1120,10 @@ extern "C" size_t sldm_gemm_tn_workspace_bytes(int64_t num_rows, int64_t mo, int
   return need;
 }
 
-extern "C" int sldm_gemm_tn(int dtype, const void* a, int64_t lda, int64_t mo, const void* b0,
-                            int64_t ldb0, int64_t n0, const void* b1, int64_t ldb1, int64_t n1,
-                            int64_t num_rows, float* out, void* workspace, size_t ws_bytes,
-                            void* stream_) {
+namespace {
+int gemm_tn_impl(int dtype, const void* a, int64_t lda, int64_t mo, const void* b0, int64_t ldb0,
+                 int64_t n0, const void* b1, int64_t ldb1, int64_t n1, int64_t num_rows,
+                 float* out, float* out1, void* workspace, size_t ws_bytes, void* stream_) {
   SLDM_REQUIRE(dtype == SLDM_F32 || dtype == SLDM_BF16, "sldm_gemm_tn: dtype %d", dtype);
   SLDM_REQUIRE(mo > 0 && n0 >= 0 && n1 >= 0 && n0 + n1 > 0 && num_rows >= 0,
                "sldm_gemm_tn: bad sizes");
@@ -1121,7 +1131,12 @@ extern "C" int sldm_gemm_tn(int dtype, const void* a, int64_t lda, int64_t mo, c
   hipStream_t stream = sldm::as_stream(stream_);
   const int64_t nn = n0 + n1;
   if (num_rows == 0) {
-    SLDM_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * (size_t)(mo * nn), stream));
+    if (out1) {
+      SLDM_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * (size_t)(mo * n0), stream));
+      SLDM_HIP_CHECK(hipMemsetAsync(out1, 0, sizeof(float) * (size_t)(mo * n1), stream));
+    } else {
+      SLDM_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * (size_t)(mo * nn), stream));
+    }
     return SLDM_OK;
   }
   const size_t need = sldm_gemm_tn_workspace_bytes(num_rows, mo, nn);
@@ -1135,7 +1150,7 @@ extern "C" int sldm_gemm_tn(int dtype, const void* a, int64_t lda, int64_t mo, c
     if (rc != SLDM_OK) return rc;
     const int64_t n = mo * nn;
     slab_reduce_kernel<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, stream>>>(
-        slab, splits, n, out);
+        slab, splits, n, out, out1, n0, nn);
     SLDM_LAUNCH_CHECK("slab_reduce_kernel");
     return SLDM_OK;
   }
@@ -1161,11 +1176,29 @@ extern "C" int sldm_gemm_tn(int dtype, const void* a, int64_t lda, int64_t mo, c
     SLDM_LAUNCH_CHECK("gemm_tn_kernel");
     const int64_t n = mo * nn;
     slab_reduce_kernel<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, stream>>>(
-        slab, pl.splits, n, out);
+        slab, pl.splits, n, out, out1, n0, nn);
     SLDM_LAUNCH_CHECK("slab_reduce_kernel");
     return SLDM_OK;
   };
   return dtype == SLDM_F32 ? run((float*)nullptr) : run((uint16_t*)nullptr);
+}
+}  // namespace
+
+extern "C" int sldm_gemm_tn(int dtype, const void* a, int64_t lda, int64_t mo, const void* b0,
+                            int64_t ldb0, int64_t n0, const void* b1, int64_t ldb1, int64_t n1,
+                            int64_t num_rows, float* out, void* workspace, size_t ws_bytes,
+                            void* stream_) {
+  return gemm_tn_impl(dtype, a, lda, mo, b0, ldb0, n0, b1, ldb1, n1, num_rows, out, nullptr,
+                      workspace, ws_bytes, stream_);
+}
+
+extern "C" int sldm_gemm_tn_split(int dtype, const void* a, int64_t lda, int64_t mo,
+                                  const void* b0, int64_t ldb0, int64_t n0, const void* b1,
+                                  int64_t ldb1, int64_t n1, int64_t num_rows, float* out0,
+                                  float* out1, void* workspace, size_t ws_bytes, void* stream_) {
+  SLDM_REQUIRE(n0 > 0 && n1 > 0 && out0 && out1, "sldm_gemm_tn_split: needs n0, n1 > 0 and both outputs");
+  return gemm_tn_impl(dtype, a, lda, mo, b0, ldb0, n0, b1, ldb1, n1, num_rows, out0, out1,
+                      workspace, ws_bytes, stream_);
 }
 
 namespace sldm {

@@ -59,6 +59,9 @@ _SIGNATURES = {
     "sldm_gemm_tn": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64,
                                     _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, ctypes.c_size_t,
                                     _vp]),
+    "sldm_gemm_tn_split": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _c_i64, _vp, _c_i64,
+                                          _c_i64, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp,
+                                          ctypes.c_size_t, _vp]),
     "sldm_gather_post_bwd_num_partials": (ctypes.c_int, [_c_i64, _c_i64]),
     "sldm_gather_post_bwd": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _vp, _vp, _vp, _vp, _c_i64,
                                             _c_i64, _c_i64, _vp, _vp, _vp, _vp, ctypes.c_float,

@@ -45,7 +45,6 @@ def sage_linear_bwd_data(dh: torch.Tensor, wl: torch.Tensor, wr: torch.Tensor,
 
 
 def sage_linear_bwd_weight(dh: torch.Tensor, agg: torch.Tensor, x: torch.Tensor):
-    """(dW_l, dW_r) = (dh^T · agg, dh^T · x), fp32."""
-    fi = x.size(1)
-    dw = ops.gemm_tn(dh, agg, x)
-    return dw[:, :fi].contiguous(), dw[:, fi:].contiguous()
+    """(dW_l, dW_r) = (dh^T · agg, dh^T · x), fp32, one launch + its reduce
+    writing both (no slicing copies)."""
+    return ops.gemm_tn(dh, agg, x, split=True)

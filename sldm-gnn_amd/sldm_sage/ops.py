@@ -299,18 +299,31 @@ def gemm_nt_rowscale(a: torch.Tensor, b: torch.Tensor, rowptr: torch.Tensor | No
     return (out, out2) if split else out
 
 
-def gemm_tn(a: torch.Tensor, b0: torch.Tensor, b1: torch.Tensor | None) -> torch.Tensor:
-    """fp32 [a.size(1), b0.size(1)+b1.size(1)] = a^T · [b0 | b1] (sum over rows)."""
+def gemm_tn(a: torch.Tensor, b0: torch.Tensor, b1: torch.Tensor | None, split: bool = False):
+    """fp32 [a.size(1), b0.size(1)+b1.size(1)] = a^T · [b0 | b1] (sum over rows).
+
+    ``split``: return (a^T b0, a^T b1) as two contiguous tensors written by the
+    same launch (``sldm_gemm_tn_split``), the layer's (dW_l, dW_r)."""
     dev = _require_gpu(a, b0, b1)
     assert a.stride(1) == 1 and b0.stride(1) == 1 and (b1 is None or b1.stride(1) == 1)
     rows, mo = a.shape
     n0 = b0.size(1)
     n1 = 0 if b1 is None else b1.size(1)
+    if split and not (n0 and n1):
+        raise ValueError("gemm_tn(split=True) needs two non-empty operands")
     lib = _lib.load()
-    out = torch.empty(mo, n0 + n1, dtype=torch.float32, device=dev)
     ws_bytes = lib.sldm_gemm_tn_workspace_bytes(rows, mo, n0 + n1)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     with _Timed("dense_bwd_weight", rows * (mo + n0 + n1) * a.element_size()):
+        if split:
+            out0 = torch.empty(mo, n0, dtype=torch.float32, device=dev)
+            out1 = torch.empty(mo, n1, dtype=torch.float32, device=dev)
+            _lib.check(lib.sldm_gemm_tn_split(
+                dtype_code(a), a.data_ptr(), a.stride(0), mo, b0.data_ptr(), b0.stride(0), n0,
+                b1.data_ptr(), b1.stride(0), n1, rows, out0.data_ptr(), out1.data_ptr(),
+                ws.data_ptr(), ws_bytes, _stream(dev)), "sldm_gemm_tn_split")
+            return out0, out1
+        out = torch.empty(mo, n0 + n1, dtype=torch.float32, device=dev)
         _lib.check(lib.sldm_gemm_tn(
             dtype_code(a), a.data_ptr(), a.stride(0), mo, b0.data_ptr(), b0.stride(0), n0,
             _ptr(b1), b1.stride(0) if b1 is not None else 0, n1, rows, out.data_ptr(),

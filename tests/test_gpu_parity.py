@@ -720,6 +720,30 @@ def test_stream_dense_fwd_vs_torch_and_mask(m, fi, kernel, monkeypatch):
     torch.testing.assert_close(rstd, rs.squeeze(1), atol=1e-3, rtol=1e-3)
 
 
+@pytest.mark.parametrize("dtype,rows,mo,n0,n1", [
+    (torch.float32, 1000, 16, 16, 16),        # C1-like: sub-tiles past the output skipped
+    (torch.float32, 8000, 96, 128, 128),      # vehicle layer shape (short node dimension)
+    (torch.float32, 70000, 128, 128, 128),    # C2-like (long node dimension plan)
+    (torch.bfloat16, 5000, 256, 256, 256),    # gemm_tn_dma.hip path
+])
+def test_gemm_tn_split_outputs_bit_equal(dtype, rows, mo, n0, n1):
+    """sldm_gemm_tn_split (dW_l, dW_r written by the reduce directly) equals
+    the column blocks of sldm_gemm_tn bit for bit, and both match torch."""
+    from sldm_sage import ops
+    gen = torch.Generator(device=DEV).manual_seed(rows + mo)
+    a = torch.randn(rows, mo, generator=gen, device=DEV).to(dtype)
+    b0 = torch.randn(rows, n0, generator=gen, device=DEV).to(dtype)
+    b1 = torch.randn(rows, n1, generator=gen, device=DEV).to(dtype)
+    whole = ops.gemm_tn(a, b0, b1)
+    d0, d1 = ops.gemm_tn(a, b0, b1, split=True)
+    torch.cuda.synchronize()
+    assert d0.is_contiguous() and d1.is_contiguous()
+    assert torch.equal(d0, whole[:, :n0]) and torch.equal(d1, whole[:, n0:])
+    ref = a.double().t() @ torch.cat([b0, b1], 1).double()
+    scale = max(1.0, float(rows) ** 0.5)
+    torch.testing.assert_close(whole.double() / scale, ref / scale, atol=1e-4, rtol=1e-4)
+
+
 @pytest.mark.parametrize("rows", [1, 31, 32, 33, 1000, 70_001, 2_000_003])
 @pytest.mark.parametrize("n1", [0, 256])
 def test_tn_dma_weight_grad_vs_torch(rows, n1, monkeypatch):
