@@ -68,6 +68,15 @@ def _ptr(t: torch.Tensor | None) -> int | None:
     return None if t is None else t.data_ptr()
 
 
+def _f32(t: torch.Tensor | None) -> torch.Tensor | None:
+    """An fp32 contiguous view of a small parameter (bias / gamma / beta) for
+    its device pointer; the parameter itself when it already is one (the
+    common case: no detach / copy per launch)."""
+    if t is None or (t.dtype == torch.float32 and t.is_contiguous()):
+        return t
+    return t.detach().float().contiguous()
+
+
 class _Timed:
     """Brackets one launch with HIP events when the timing hook is set."""
 
@@ -259,8 +268,7 @@ def sage_dense_fwd(agg: torch.Tensor, x: torch.Tensor, wcat: torch.Tensor, bias,
         out = torch.empty(n, fo, dtype=x.dtype, device=dev)
         xhat = torch.empty(n, fo, dtype=x.dtype, device=dev) if save else None
         rstd = torch.empty(n, dtype=torch.float32, device=dev) if save else None
-    f32 = lambda t: None if t is None else t.detach().float().contiguous()  # noqa: E731
-    bias_, gamma_, beta_ = f32(bias), f32(gamma), f32(beta)
+    bias_, gamma_, beta_ = _f32(bias), _f32(gamma), _f32(beta)
     s = x.element_size()
     with _Timed("dense_fwd", (2 * n * fi + n * fo * (2 if save else 1)) * s):
         _lib.check(_lib.load().sldm_sage_dense_fwd(
@@ -342,8 +350,7 @@ def post_fwd(h: torch.Tensor, bias, gamma, beta, eps: float, slope: float, drop_
     out = torch.empty(N, F, dtype=out_dtype, device=dev)
     xhat = torch.empty(N, F, dtype=out_dtype, device=dev) if save else None
     rstd = torch.empty(N, dtype=torch.float32, device=dev) if save else None
-    f32 = lambda t: None if t is None else t.detach().float().contiguous()  # noqa: E731
-    bias_, gamma_, beta_ = f32(bias), f32(gamma), f32(beta)
+    bias_, gamma_, beta_ = _f32(bias), _f32(gamma), _f32(beta)
     with _Timed("post_fwd", N * F * (h.element_size() + out.element_size() * (2 if save else 1))):
         _lib.check(_lib.load().sldm_post_fwd(
             dtype_code(h), h.data_ptr(), h.stride(0), N, F, _ptr(bias_), gamma_.data_ptr(),
@@ -370,8 +377,7 @@ def gather_post_bwd(g: torch.Tensor, t_rowptr: torch.Tensor, t_col: torch.Tensor
     dh = torch.empty(N, F, dtype=xhat.dtype, device=dev)
     partials = torch.empty(np_, 3 * F, dtype=torch.float32, device=dev)
     cols = torch.empty(3 * F, dtype=torch.float32, device=dev)
-    gamma_ = gamma.detach().float().contiguous()
-    beta_ = beta.detach().float().contiguous()
+    gamma_, beta_ = _f32(gamma), _f32(beta)
     s = xhat.element_size()
     E = t_col.numel()
     with _Timed("gather_post_bwd", E * (4 + F * s) + (N + 1) * 4 + 3 * N * F * s + 4 * N):
@@ -453,8 +459,7 @@ def post_bwd(dout: torch.Tensor, xhat: torch.Tensor, rstd: torch.Tensor, gamma, 
     dh = torch.empty(N, F, dtype=dh_dtype, device=dev)
     partials = torch.empty(np_, 3 * F, dtype=torch.float32, device=dev)
     cols = torch.empty(3 * F, dtype=torch.float32, device=dev)
-    gamma_ = gamma.detach().float().contiguous()
-    beta_ = beta.detach().float().contiguous()
+    gamma_, beta_ = _f32(gamma), _f32(beta)
     with _Timed("post_bwd", N * F * ((3 if zout is not None else 2) * xhat.element_size()
                                      + dh.element_size())):
         _lib.check(lib.sldm_post_bwd(
