@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SLDM_ABI_VERSION 5
+#define SLDM_ABI_VERSION 6   /* 6: + sldm_gemm_tn_split */
 
 enum sldm_dtype { SLDM_F32 = 0, SLDM_BF16 = 1 };
 enum sldm_status { SLDM_OK = 0, SLDM_ERR_ARG = 1, SLDM_ERR_HIP = 2 };

@@ -15,7 +15,7 @@ import torch  # noqa: F401  (must be imported before the HIP library)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SLDM_SAGE_LIB", os.path.join(_HERE, "libsldm_sage.so"))
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 F32, BF16 = 0, 1
 
 _c_i64 = ctypes.c_int64
