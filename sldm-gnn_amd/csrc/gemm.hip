@@ -25,8 +25,6 @@
 //   panels hit that XCD's L2; fp32 partial slabs are summed in a fixed order.
 #include "common.hpp"
 
-#include <type_traits>
-
 namespace {
 
 typedef short s8v __attribute__((ext_vector_type(8)));
@@ -832,12 +830,6 @@ __global__ __launch_bounds__(kBlock) void gemm_tn_kernel(TnArgs<T> p) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int q = lane >> 4, r16 = lane & 15;
   const int wm = wave >> 1, wn = wave & 1;   // 2 x 2 waves, 64 x 64 each
-  // 16 x 16 sub-tiles of this wave inside [mo) x [nn) (wave-uniform): the
-  // MFMAs of sub-tiles wholly past the output are skipped (narrow layers, e.g.
-  // F = 16: 2 of the tile's 64 sub-tiles are real)
-  const int mi = __builtin_amdgcn_readfirstlane(min(4, max(0, (p.mo - mbase - wm * 64 + 15) / 16)));
-  const int nj = __builtin_amdgcn_readfirstlane(min(4, max(0, (p.nn - nbase - wn * 64 + 15) / 16)));
-  const bool full_tile = mi == 4 && nj == 4;
 
   f4v acc[4][4];
 #pragma unroll
@@ -885,15 +877,11 @@ __global__ __launch_bounds__(kBlock) void gemm_tn_kernel(TnArgs<T> p) {
             (__attribute__((address_space(3))) s4v*)(pb + 4 * PITCH));
         bf[i] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
-      auto mma = [&](auto full) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (decltype(full)::value || (i < mi && j < nj))
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
-      };
-      if (full_tile) mma(std::true_type{}); else mma(std::false_type{});
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
      }
     } else {
 #pragma unroll
@@ -904,15 +892,11 @@ __global__ __launch_bounds__(kBlock) void gemm_tn_kernel(TnArgs<T> p) {
           af[i] = reinterpret_cast<const float*>(lds_a)[(kk + q) * PITCH + wm * 64 + 16 * i + r16];
           bf[i] = reinterpret_cast<const float*>(lds_b)[(kk + q) * PITCH + wn * 64 + 16 * i + r16];
         }
-        auto mma = [&](auto full) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (decltype(full)::value || (i < mi && j < nj))
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
-        };
-        if (full_tile) mma(std::true_type{}); else mma(std::false_type{});
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
       }
     }
   }
