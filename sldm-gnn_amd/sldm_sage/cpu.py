@@ -114,8 +114,10 @@ class _CpuLayerFn(torch.autograd.Function):
         out = torch.empty(n, fo)
         xhat = torch.empty(n, fo)
         rstd = torch.empty(n)
-        load().sldm_cpu_post_fwd(h.data_ptr(), fo, n, fo, _p(_f32(bl)), _f32(gamma).data_ptr(),
-                                 _f32(beta).data_ptr(), float(eps), float(slope), float(drop_p),
+        # bound to locals: a converted copy must outlive the C call
+        bias_, gamma_, beta_ = _f32(bl), _f32(gamma), _f32(beta)
+        load().sldm_cpu_post_fwd(h.data_ptr(), fo, n, fo, _p(bias_), gamma_.data_ptr(),
+                                 beta_.data_ptr(), float(eps), float(slope), float(drop_p),
                                  seed & (2**64 - 1), 0, out.data_ptr(), xhat.data_ptr(),
                                  rstd.data_ptr())
         ctx.save_for_backward(x, agg, xhat, rstd, wl, wr, gamma, beta)
@@ -131,8 +133,9 @@ class _CpuLayerFn(torch.autograd.Function):
         dout = dout.float().contiguous()
         dh = torch.empty(n, fo)
         dg, db, dbias = torch.empty(fo), torch.empty(fo), torch.empty(fo)
+        gamma_, beta_ = _f32(gamma), _f32(beta)
         load().sldm_cpu_post_bwd(dout.data_ptr(), xhat.data_ptr(), rstd.data_ptr(), n, fo,
-                                 _f32(gamma).data_ptr(), _f32(beta).data_ptr(), float(slope),
+                                 gamma_.data_ptr(), beta_.data_ptr(), float(slope),
                                  float(drop_p), seed & (2**64 - 1), 0, dh.data_ptr(),
                                  dg.data_ptr(), db.data_ptr(), dbias.data_ptr())
         dwl = torch.mm(dh.t(), agg)

@@ -222,7 +222,11 @@ class PackDataset(torch.utils.data.Dataset):
             for i in range(self.len()):
                 g = self.innerGet(i)
                 pres = g.x[:, :, -1] > 0.5                       # [V, T]
-                feats = g.x[:, :, :-1] * pres[:, :, None]        # absent frames add 0
+                # absent frames are dropped, whatever they hold (the reference
+                # indexes them away, dataset.py:127-131: a NaN / inf there must
+                # not reach the sums)
+                feats = torch.where(pres[:, :, None], g.x[:, :, :-1],
+                                    torch.zeros((), dtype=g.x.dtype, device=g.x.device))
                 sum_x += feats.sum(dim=(0, 1), keepdim=True)
                 sum_x2 += (feats ** 2).sum(dim=(0, 1), keepdim=True)
                 tot_cnt += int(pres.sum())

@@ -855,7 +855,7 @@ class DistSageBlock(nn.Module):
         return "feature" if isinstance(self.part, FeaturePartition) else "halo"
 
     def forward(self, x_local: torch.Tensor) -> torch.Tensor:
-        from .sageblock import _act_slope, _drop_p, _new_seed
+        from .sageblock import _act_slope, _cpu_seed, _drop_p, _new_seed
         if isinstance(self.part, ReplicaPartition):
             # every rank runs the whole block: gradients are complete and
             # identical on every rank, nothing crosses xGMI
@@ -867,7 +867,11 @@ class DistSageBlock(nn.Module):
         for i, (conv, post) in enumerate(layers):
             ln, act, drop = post[0], post[1], post[2]
             p = _drop_p(drop)
-            seed = _new_seed(x.device) if p > 0 else 0
+            # CPU tensors (the gloo / host-backend path) draw from torch's CPU
+            # generator, as SageBlock's CPU mode does; the device generator
+            # would need (and initialise) a GPU
+            seed = 0 if p <= 0 else (_cpu_seed() if x.device.type == "cpu"
+                                     else _new_seed(x.device))
             args = (x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, ln.weight, ln.bias,
                     self.part, self.group, self.backend, _act_slope(act), p, seed, float(ln.eps))
             if feat:
@@ -949,14 +953,17 @@ def measure_link_bps(device: torch.device, group=None, per_peer_bytes: int = 32 
 
 
 def estimate_strategies(edge_index: torch.Tensor, num_nodes: int, world: int, rank: int,
-                        feat: int, elem: int, group=None, link_bps: float | None = None) -> dict:
+                        feat: int, elem: int, group=None, link_bps: float | None = None,
+                        balance: str = "cost") -> dict:
     """Modelled per-layer time (s) of the halo, feature-sliced and replicated
     strategies: exchange bytes / xGMI + gather bytes / measured gather rate +
     dense bytes / stream rate, max over ranks (collective over ``group`` when
     world > 1, so every rank gets the same numbers).  ``link_bps``: the
     per-peer xGMI rate to price exchanges at (:func:`measure_link_bps`;
-    default ``_LINK_BPS``)."""
-    hb_ = row_bounds(edge_index, num_nodes, world, "cost")     # partition_graph's blocks
+    default ``_LINK_BPS``).  ``balance``: the row-block rule the halo strategy
+    would be built with ("cost" or "rows"), so the model prices the blocks
+    :func:`partition_graph` cuts."""
+    hb_ = row_bounds(edge_index, num_nodes, world, balance)    # partition_graph's blocks
     h0, h1 = hb_[rank], hb_[rank + 1]
     src, dst = edge_index[0], edge_index[1]
     in_mask = (dst >= h0) & (dst < h1)
@@ -1045,7 +1052,7 @@ def plan_partition(edge_index: torch.Tensor, num_nodes: int, world: int, rank: i
         else:
             _trace("plan: estimate")
             info = estimate_strategies(edge_index, num_nodes, world, rank, feat, elem, group,
-                                       link_bps)
+                                       link_bps, balance)
             _trace("plan: estimated")
             strategy = choose_strategy(info)
     info["strategy"] = strategy

@@ -37,9 +37,15 @@ def _ptr(t):
 
 
 class _GruFn(torch.autograd.Function):
+    last_backward_had_dout: bool | None = None
+
     @staticmethod
     def forward(ctx, x, h0, w_ih, w_hh, b_ih, b_hh, batch_first: bool):
         dev = _require_gpu(x, h0, w_ih, w_hh, b_ih, b_hh)
+        # an output nobody differentiates (GruSage reads only hlast,
+        # grusage.py:160-161) reaches backward as None, not as an [N, T, H]
+        # tensor of zeros the kernel would stream every step
+        ctx.set_materialize_grads(False)
         for name, t in (("input", x), ("h0", h0), ("weight", w_ih), ("weight", w_hh),
                         ("bias", b_ih), ("bias", b_hh)):
             if t is not None and t.dtype != torch.float32:
@@ -84,6 +90,7 @@ class _GruFn(torch.autograd.Function):
         batch_first, N, T, I, H, (ldxn, ldxt), (ldon, ldot), has_bih, has_bhh = ctx.cfg
         dev = x.device
         lib = _lib.load()
+        _GruFn.last_backward_had_dout = dout is not None     # observed by the tests
         if dout is not None:
             dout = dout if dout.stride(-1) == 1 else dout.contiguous()
             lddn, lddt = (dout.stride(0), dout.stride(1)) if batch_first else (dout.stride(1),

@@ -8,7 +8,35 @@ The product never uses it.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
+
+
+def _hash32(x):
+    x = x.astype(np.uint32)
+    x ^= x >> np.uint32(16)
+    x *= np.uint32(0x7FEB352D)
+    x ^= x >> np.uint32(15)
+    x *= np.uint32(0x846CA68B)
+    x ^= x >> np.uint32(16)
+    return x
+
+
+def dropout_keep(seed: int, row0: int, rows: int, feat: int, p: float) -> torch.Tensor:
+    """The kernels' counter-hash dropout mask, restated (csrc/common.hpp:
+    dropout_row_key / dropout_keep): keep[i, j] for global rows row0 + i."""
+    with np.errstate(over="ignore"):
+        r = np.arange(row0, row0 + rows, dtype=np.uint64)
+        lo, hi = np.uint32(seed & 0xFFFFFFFF), np.uint32((seed >> 32) & 0xFFFFFFFF)
+        inner = hi ^ _hash32((r & np.uint64(0xFFFFFFFF)).astype(np.uint32)) ^ (
+            (r >> np.uint64(32)).astype(np.uint32) * np.uint32(0x9E3779B9))
+        key = _hash32(lo ^ _hash32(inner))
+        col = np.arange(feat, dtype=np.uint32)
+        h = _hash32(key[:, None] + (col >> np.uint32(1))[None, :] * np.uint32(0x9E3779B9))
+        v = np.where((col & np.uint32(1))[None, :] == 1, h >> np.uint32(16), h & np.uint32(0xFFFF))
+    thr = 65536 if p >= 1 else (0 if p <= 0 else int(np.float32(p) * np.float32(65536.0)
+                                                   + np.float32(0.5)))
+    return torch.from_numpy(v >= thr)
 
 
 class CpuBackend:
@@ -61,7 +89,8 @@ class CpuBackend:
     @staticmethod
     def layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p, seed, save, row_offset,
                   outs=None):
-        res = CpuBackend._layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p)
+        res = CpuBackend._layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p, seed,
+                                    row_offset)
         if outs is None:
             return res
         for dst, src in zip(outs, res):
@@ -70,19 +99,27 @@ class CpuBackend:
         return outs
 
     @staticmethod
-    def _layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p):
-        assert drop_p == 0.0, "CPU test backend has no dropout"
+    def _layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope, drop_p, seed=0, row_offset=0):
         h = agg @ wl.detach().t() + bl.detach() + x @ wr.detach().t()
         mu = h.mean(1, keepdim=True)
         rstd = 1.0 / torch.sqrt(((h - mu) ** 2).mean(1, keepdim=True) + eps)
         xhat = (h - mu) * rstd
         y = xhat * gamma.detach() + beta.detach()
         out = torch.where(y > 0, y, y * slope)
+        if drop_p > 0:
+            keep = dropout_keep(seed, row_offset, out.size(0), out.size(1), drop_p)
+            out = torch.where(keep, out * (1.0 / (1.0 - drop_p)), torch.zeros(()))
         return out, xhat, rstd.squeeze(1)
 
     @staticmethod
     def post_bwd(dout, xhat, rstd, gamma, beta, slope, drop_p, seed, zout, row_offset):
-        dy = torch.where(zout > 0, dout, dout * slope)
+        if drop_p > 0:
+            keep = dropout_keep(seed, row_offset, dout.size(0), dout.size(1), drop_p)
+            dout = torch.where(keep, dout * (1.0 / (1.0 - drop_p)), torch.zeros(()))
+            y = xhat * gamma.detach() + beta.detach()       # dropped outputs lost their sign
+            dy = torch.where(y > 0, dout, dout * slope)
+        else:
+            dy = torch.where(zout > 0, dout, dout * slope)
         gx = dy * gamma.detach()
         r = rstd[:, None]
         dh = r * (gx - gx.mean(1, keepdim=True) - xhat * (gx * xhat).mean(1, keepdim=True))

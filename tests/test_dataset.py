@@ -70,10 +70,17 @@ def _install_fake_pyg():
 
 
 def _pack(n, e, T, seed):
-    """A pack like gbuilder.py:115-131 emits (x [n, T, 6] with presence last)."""
+    """A pack like gbuilder.py:115-131 emits (x [n, T, 6] with presence last).
+    Pack 3 holds NaN / inf in some absent frames: the statistics must ignore
+    them, as the reference's boolean indexing does (dataset.py:127-131)."""
     g = torch.Generator().manual_seed(seed)
     x = torch.randn(n, T, 6, generator=g)
     x[:, :, -1] = (torch.rand(n, T, generator=g) > 0.3).float()
+    if seed == 3:
+        absent = x[:, :, -1] < 0.5
+        assert bool(absent.any())
+        junk = torch.tensor([float("nan"), float("inf")])[torch.arange(int(absent.sum())) % 2]
+        x[:, :, 0][absent] = junk
     return dict(x=x, xsttype=torch.randint(0, 256, (n,), generator=g),
                 xdims=torch.rand(n, 2, generator=g) * 4,
                 edge_index=torch.randint(0, n, (2, e), generator=g),

@@ -51,7 +51,7 @@ def _graph(kind, n, e, f):
 
 
 def _worker(rank, world, port, hdims, n, e, q, strategy="halo", chunks=4, graph="random",
-            balance="cost"):
+            balance="cost", dropout=None, train=True):
     sys.path[:0] = [HERE, os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "sldm-gnn_amd")]
     import torch.distributed as dist
 
@@ -68,8 +68,23 @@ def _worker(rank, world, port, hdims, n, e, q, strategy="halo", chunks=4, graph=
         gout = torch.randn(n, hdims[-1], generator=torch.Generator().manual_seed(4))
         ref = oracle_block(hdims, 0.1)
         out_r, dx_r, grads_r = run_oracle(ref, x, ei, gout)
+        if dropout is not None and train:
+            # training-mode masks: the reference is the single-process SageBlock
+            # on CPU tensors (host kernels, same counter hash), its dropout
+            # keys drawn from torch's CPU generator in the same order
+            one = SageBlock(hdims, dropout, 0.1)
+            one.load_state_dict(ref.state_dict())
+            xf = x.clone().requires_grad_(True)
+            torch.manual_seed(123)
+            o = one(xf, ei)
+            o.backward(gout)
+            out_r, dx_r = o.detach(), xf.grad
+            grads_r = {k: p.grad for k, p in one.named_parameters()}
+            zeros = float((out_r == 0).float().mean())
+            assert abs(zeros - dropout) < 0.05, zeros
 
-        blk = SageBlock(hdims, None, 0.1)
+        blk = SageBlock(hdims, dropout, 0.1)
+        blk.train(train)
         if rank == 0:
             blk.load_state_dict(ref.state_dict())   # other ranks get it by broadcast
         part, info = plan_partition(ei, n, world, rank, hdims[0], 4, strategy=strategy,
@@ -88,6 +103,7 @@ def _worker(rank, world, port, hdims, n, e, q, strategy="halo", chunks=4, graph=
         model = DistSageBlock(blk, part, backend=CpuBackend)
         r0, r1 = part.row_begin, part.row_end
         xl = x[r0:r1].clone().requires_grad_(True)
+        torch.manual_seed(123)
         out = model(xl)
         out.backward(gout[r0:r1])
         tol = dict(atol=1e-5, rtol=1e-5)
@@ -104,13 +120,14 @@ def _worker(rank, world, port, hdims, n, e, q, strategy="halo", chunks=4, graph=
         dist.destroy_process_group()
 
 
-def _run(world, n, hdims, strategy, chunks=4, graph="random", balance="cost"):
+def _run(world, n, hdims, strategy, chunks=4, graph="random", balance="cost", dropout=None,
+         train=True):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker,
                          args=(r, world, port, hdims, n, 6 * n, q, strategy, chunks, graph,
-                               balance))
+                               balance, dropout, train))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -124,6 +141,15 @@ def _run(world, n, hdims, strategy, chunks=4, graph="random", balance="cost"):
 @pytest.mark.parametrize("world,n", [(2, 300), (3, 301), (4, 97), (8, 203)])
 def test_dist_sageblock_matches_single_device(world, n):
     _run(world, n, [8, 12, 8], "halo")
+
+
+@pytest.mark.parametrize("strategy", ["halo", "feature"])
+@pytest.mark.parametrize("train", [False, True])
+def test_dist_sageblock_dropout_on_cpu_tensors(strategy, train):
+    """Dropout > 0 on CPU tensors: the layer keys come from torch's CPU
+    generator (no GPU needed or initialised); eval mode equals the oracle,
+    training mode draws the single-process mask (global row ids)."""
+    _run(2, 150, [8, 12, 8], strategy, dropout=0.25, train=train)
 
 
 def test_halo_closed_component_rank_joins_exchange():

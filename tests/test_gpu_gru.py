@@ -79,8 +79,15 @@ def test_gru_time_major_h0_no_bias():
 
 
 def test_gru_only_h_n_gradient():
-    """GruSage reads only hlast[-1] (grusage.py:160-161): no output gradient."""
+    """GruSage reads only hlast[-1] (grusage.py:160-161): no output gradient.
+    The backward must then receive dout = None (the kernel's no-dout path),
+    not a materialised [N, T, H] tensor of zeros."""
+    from sldm_sage import gru as gru_mod
+    gru_mod._GruFn.last_backward_had_dout = None
     _run_pair(64, 20, 6, 96, gout=False, dx=False)
+    assert gru_mod._GruFn.last_backward_had_dout is False
+    _run_pair(64, 20, 6, 96, gout=True, dx=False)
+    assert gru_mod._GruFn.last_backward_had_dout is True
 
 
 def test_gru_model_shape():
