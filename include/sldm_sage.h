@@ -17,7 +17,8 @@
  *   - dtype codes: SLDM_F32 (fp32) and SLDM_BF16 (bf16 storage, fp32 math);
  *   - return value: SLDM_OK or an error code; sldm_last_error() then returns a
  *     thread-local message.  Launch failures are reported from hipGetLastError.
- *   - thread safety: no global mutable state; safe from any host thread.
+ *   - thread safety: safe from any host thread; the only global state is the
+ *     per-device address of sldm_gather_rows_split_static's scratch array.
  */
 #ifndef SLDM_SAGE_H
 #define SLDM_SAGE_H
@@ -29,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SLDM_ABI_VERSION 6   /* 6: + sldm_gemm_tn_split */
+#define SLDM_ABI_VERSION 7   /* 7: + sldm_gather_rows_split_static */
 
 enum sldm_dtype { SLDM_F32 = 0, SLDM_BF16 = 1 };
 enum sldm_status { SLDM_OK = 0, SLDM_ERR_ARG = 1, SLDM_ERR_HIP = 2 };
@@ -104,6 +105,28 @@ int sldm_gather_rows_split(int x_dtype, const void* x, int64_t ldx,
                            int64_t num_hubs, const int32_t* chunk_row, const int32_t* chunk_beg,
                            int64_t num_chunks, int32_t chunk_len, int32_t max_deg,
                            float* partials, void* stream);
+
+/* sldm_gather_rows_split without a workspace argument and without any device
+ * allocation.  No counterpart in the reference: it exists for callers that
+ * cannot allocate -- code under HIP graph capture, tight serving loops,
+ * harnesses that forbid hipMalloc.  The chunk partials live in a static device
+ * array inside the library (sldm_gather_rows_split_static_max_floats() floats
+ * = 16 MiB, held by every GPU the library runs on until the process ends);
+ * num_chunks * feat beyond that is rejected with SLDM_ERR_ARG.  The device
+ * that is current at the call must be the stream's device.  All calls on one
+ * GPU share the array: calls that overlap on one GPU (two streams, two host
+ * threads) race; serialise them or use sldm_gather_rows_split.  Same results,
+ * bit for bit, as sldm_gather_rows_split. */
+size_t sldm_gather_rows_split_static_max_floats(void);
+int sldm_gather_rows_split_static(int x_dtype, const void* x, int64_t ldx,
+                                  const int32_t* rowptr, const int32_t* col,
+                                  const int32_t* row_order, int64_t num_rows, int64_t feat,
+                                  int mean, const void* addend, int64_t ld_add, int out_dtype,
+                                  void* out, int64_t ldo, const int32_t* hub_rows,
+                                  const int32_t* hub_chunk_ptr, int64_t num_hubs,
+                                  const int32_t* chunk_row, const int32_t* chunk_beg,
+                                  int64_t num_chunks, int32_t chunk_len, int32_t max_deg,
+                                  void* stream);
 
 /* g[i,:] = d[i,:] / max(1, rowptr[i+1]-rowptr[i]), in place, dtype of d.
  * Backward of the mean's division (A8) folded before the transpose sum. */

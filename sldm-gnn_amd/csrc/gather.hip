@@ -34,6 +34,8 @@
 // divides by the degree, adds the addend and stores the row.
 #include "common.hpp"
 
+#include <mutex>
+
 namespace {
 
 constexpr int kBlock = 256;
@@ -381,6 +383,65 @@ extern "C" int sldm_gather_rows_split(int x_dtype, const void* x, int64_t ldx,
              hub_chunk_ptr, num_hubs};
   return gather_rows_impl(x_dtype, x, ldx, rowptr, col, row_order, num_rows, feat, mean, addend,
                           ld_add, out_dtype, out, ldo, hp, stream_);
+}
+
+// ------------------------------------------------ no-allocation variant --
+// sldm_gather_rows_split for callers that cannot allocate device memory (code
+// under HIP graph capture, tight serving loops): the chunk partials live in
+// `scratch`, a file-scope device array of kStaticPartialFloats floats that each
+// GPU the library runs on holds until the process ends.  Host code never
+// passes the array's name to a kernel (on the host it is only a stand-in for
+// the symbol): the device address comes from hipGetSymbolAddress, once per
+// device with that device current, and is kept per device.
+namespace {
+constexpr size_t kStaticPartialFloats = (size_t)4 << 20;          // 16 MiB
+static __device__ __align__(256) float scratch[kStaticPartialFloats];
+constexpr int kMaxDevices = 64;
+float* g_scratch_ptr[kMaxDevices] = {};
+std::mutex g_scratch_mu;
+
+// Device address of `scratch` on the current device (resolved on first use).
+int static_partials(float** out) {
+  int dev = -1;
+  SLDM_HIP_CHECK(hipGetDevice(&dev));
+  SLDM_REQUIRE(dev >= 0 && dev < kMaxDevices, "sldm_gather_rows_split_static: device %d", dev);
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  if (!g_scratch_ptr[dev]) {
+    float* p = nullptr;
+    SLDM_HIP_CHECK(hipGetSymbolAddress(reinterpret_cast<void**>(&p), HIP_SYMBOL(scratch)));
+    SLDM_REQUIRE(p != nullptr, "sldm_gather_rows_split_static: no device address for the scratch");
+    g_scratch_ptr[dev] = p;
+  }
+  *out = g_scratch_ptr[dev];
+  return SLDM_OK;
+}
+}  // namespace
+
+extern "C" size_t sldm_gather_rows_split_static_max_floats(void) { return kStaticPartialFloats; }
+
+extern "C" int sldm_gather_rows_split_static(
+    int x_dtype, const void* x, int64_t ldx, const int32_t* rowptr, const int32_t* col,
+    const int32_t* row_order, int64_t num_rows, int64_t feat, int mean, const void* addend,
+    int64_t ld_add, int out_dtype, void* out, int64_t ldo, const int32_t* hub_rows,
+    const int32_t* hub_chunk_ptr, int64_t num_hubs, const int32_t* chunk_row,
+    const int32_t* chunk_beg, int64_t num_chunks, int32_t chunk_len, int32_t max_deg,
+    void* stream_) {
+  SLDM_REQUIRE(num_chunks >= 0 && feat >= 0 &&
+                   (feat == 0 || (uint64_t)num_chunks <= kStaticPartialFloats / (uint64_t)feat),
+               "sldm_gather_rows_split_static: %lld chunks x %lld features exceed the static "
+               "scratch of %zu floats; use sldm_gather_rows_split with a caller workspace",
+               (long long)num_chunks, (long long)feat, kStaticPartialFloats);
+  float* partials = nullptr;
+  if (num_chunks > 0) {
+    const int rc = static_partials(&partials);
+    if (rc != SLDM_OK) return rc;
+  }
+  // every chunk slot of the launch overwrites its whole partial row before the
+  // finish kernel reads it, so nothing of the previous call's contents is read
+  return sldm_gather_rows_split(x_dtype, x, ldx, rowptr, col, row_order, num_rows, feat, mean,
+                                addend, ld_add, out_dtype, out, ldo, hub_rows, hub_chunk_ptr,
+                                num_hubs, chunk_row, chunk_beg, num_chunks, chunk_len, max_deg,
+                                partials, stream_);
 }
 
 // ------------------------------------------------------------------------

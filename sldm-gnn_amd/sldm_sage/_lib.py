@@ -15,7 +15,7 @@ import torch  # noqa: F401  (must be imported before the HIP library)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SLDM_SAGE_LIB", os.path.join(_HERE, "libsldm_sage.so"))
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 F32, BF16 = 0, 1
 
 _c_i64 = ctypes.c_int64
@@ -38,6 +38,12 @@ _SIGNATURES = {
                                               _c_i64, ctypes.c_int, _vp, _c_i64, ctypes.c_int,
                                               _vp, _c_i64, _vp, _vp, _c_i64, _vp, _vp, _c_i64,
                                               ctypes.c_int32, ctypes.c_int32, _vp, _vp]),
+    "sldm_gather_rows_split_static_max_floats": (ctypes.c_size_t, []),
+    "sldm_gather_rows_split_static": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _vp, _vp, _vp,
+                                                     _c_i64, _c_i64, ctypes.c_int, _vp, _c_i64,
+                                                     ctypes.c_int, _vp, _c_i64, _vp, _vp, _c_i64,
+                                                     _vp, _vp, _c_i64, ctypes.c_int32,
+                                                     ctypes.c_int32, _vp]),
     "sldm_scale_rows_by_inv_deg": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _vp, _c_i64,
                                                   _c_i64, _vp]),
     "sldm_post_fwd": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp,
