@@ -81,19 +81,22 @@ class HipBackend:
         return rowptr, col, t_rowptr, t_col
 
     @staticmethod
-    def gather(x, rowptr, col, num_rows, mean, addend=None, rows=None, out=None, edges=None):
+    def gather(x, rowptr, col, num_rows, mean, addend=None, rows=None, out=None, edges=None,
+               hub=None):
         """Rows ``rows`` (a :class:`RowSubset`; all rows when None) of the CSR
         gather, written into ``out`` (allocated when None).  ``edges``: the
-        edge count of a rowptr window (byte accounting only)."""
+        edge count of a rowptr window (byte accounting only).  ``hub``: the
+        high-degree split plan of all rows (a subset carries its own)."""
         from . import ops
         name = "gather_fwd" if mean else "gather_bwd"
         if rows is None:
             return ops.gather_rows(x, rowptr, col, num_rows, mean=mean, addend=addend, out=out,
-                                   name=name, edges=edges)
+                                   name=name, edges=edges, hub=hub)
         if out is None:
             out = torch.empty(num_rows, x.size(1), dtype=x.dtype, device=x.device)
         return ops.gather_rows(x, rowptr, col, rows.rows.numel(), mean=mean, addend=addend,
-                               out=out, name=name, order=rows.rows, edges=rows.edges)
+                               out=out, name=name, order=rows.rows, edges=rows.edges,
+                               hub=rows.hub)
 
     @staticmethod
     def pick_rows(x, rowptr, idx):
@@ -280,6 +283,7 @@ class HaloPlan:
 class RowSubset:
     rows: torch.Tensor            # int32 local row ids
     edges: int                    # in-edges of those rows
+    hub: object | None = None     # graph.HubPlan of the subset's high-degree rows
 
 
 @dataclass
@@ -294,12 +298,31 @@ class RowSplit:
     pending: RowSubset
 
 
-def _split_rows(g: SageGraph, n_own: int) -> RowSplit | None:
+def _hub_threshold(num_nodes: int, num_edges: int, device) -> int | None:
+    """The single-GPU path's high-degree rule (graph.build_graph) for the
+    WHOLE graph, so a partition splits exactly the rows one GPU would split,
+    into the same chunks: the W-rank sums then equal the one-GPU bits.  None:
+    no split (small graphs, the host backend's CPU tensors, SLDM_SKEW)."""
+    from . import graph as graph_mod
+    if (device.type != "cuda" or num_edges < graph_mod.HUB_MIN_EDGES
+            or graph_mod._skew_mode() != "split"):
+        return None
+    return graph_mod.hub_threshold(num_nodes, num_edges)
+
+
+def _split_rows(g: SageGraph, n_own: int, hub_thr: int | None = None) -> RowSplit | None:
+    """Rows by whether they read halo rows (None: none do).  ``hub_thr``: rows
+    above this degree are split into edge chunks (graph.hub_plan); sets
+    ``g.hub`` (all rows) and each subset's own plan."""
+    from .graph import hub_plan
     n = g.num_nodes
     if n == 0 or g.num_edges == 0:
         return None
     dev = g.rowptr.device
     deg = (g.rowptr[1:] - g.rowptr[:-1]).long()
+    skewed = hub_thr is not None and int(deg.max()) > hub_thr
+    if skewed:
+        g.hub = hub_plan(g.rowptr, hub_thr)
     row_of_edge = torch.repeat_interleave(torch.arange(n, device=dev), deg)
     halo_edge = g.col[: g.num_edges].long() >= n_own
     if not bool(halo_edge.any()):
@@ -309,8 +332,10 @@ def _split_rows(g: SageGraph, n_own: int) -> RowSplit | None:
     pend = has_halo.nonzero().squeeze(1)
     res = (~has_halo).nonzero().squeeze(1)
     pend_edges = int(deg[pend].sum())
-    return RowSplit(RowSubset(res.to(torch.int32), g.num_edges - pend_edges),
-                    RowSubset(pend.to(torch.int32), pend_edges))
+    res_hub = hub_plan(g.rowptr, hub_thr, row_mask=~has_halo) if skewed else None
+    pend_hub = hub_plan(g.rowptr, hub_thr, row_mask=has_halo) if skewed else None
+    return RowSplit(RowSubset(res.to(torch.int32), g.num_edges - pend_edges, res_hub),
+                    RowSubset(pend.to(torch.int32), pend_edges, pend_hub))
 
 
 @dataclass
@@ -421,8 +446,9 @@ def partition_graph(edge_index: torch.Tensor, num_nodes: int, world: int, rank: 
     _trace("partition_graph: split rows")
     fwd = SageGraph(n, int(ein.size(1)), rp[: n + 1], col, None, None)
     bwd = SageGraph(n, int(eout.size(1)), trp[: n + 1], tcol, None, None)
+    thr = _hub_threshold(num_nodes, int(edge_index.size(1)), edge_index.device)
     return GraphPartition(rank, world, num_nodes, bounds, r0, r1, fwd, bwd, plan_f, plan_b,
-                          _split_rows(fwd, n), _split_rows(bwd, n))
+                          _split_rows(fwd, n, thr), _split_rows(bwd, n, thr))
 
 
 def _overlapped_gather(backend, buf, work, g: SageGraph, split: RowSplit | None, num_rows,
@@ -432,7 +458,7 @@ def _overlapped_gather(backend, buf, work, g: SageGraph, split: RowSplit | None,
     if work is None or split is None:
         if work is not None:
             work.wait()
-        return backend.gather(buf, g.rowptr, g.col, num_rows, mean, addend=addend)
+        return backend.gather(buf, g.rowptr, g.col, num_rows, mean, addend=addend, hub=g.hub)
     out = backend.gather(buf, g.rowptr, g.col, num_rows, mean, addend=addend,
                          rows=split.resident)
     work.wait()

@@ -129,10 +129,16 @@ def build_graph(edge_index: torch.Tensor, num_nodes: int, transpose: bool = True
     return g
 
 
-def hub_plan(rowptr: torch.Tensor, max_deg: int, chunk_len: int = HUB_CHUNK) -> HubPlan | None:
-    """Chunk table of the rows with degree > max_deg (None if there are none)."""
+def hub_plan(rowptr: torch.Tensor, max_deg: int, chunk_len: int = HUB_CHUNK,
+             row_mask: torch.Tensor | None = None) -> HubPlan | None:
+    """Chunk table of the rows with degree > max_deg (None if there are none).
+    ``row_mask`` (bool [N]): only the hubs among these rows (a row subset's
+    plan; the launch still skips every row above max_deg)."""
     deg = (rowptr[1:] - rowptr[:-1]).long()
-    hubs = (deg > max_deg).nonzero().squeeze(1)
+    is_hub = deg > max_deg
+    if row_mask is not None:
+        is_hub &= row_mask
+    hubs = is_hub.nonzero().squeeze(1)
     nch = (deg[hubs] + chunk_len - 1) // chunk_len
     ptr = torch.zeros(hubs.numel() + 1, dtype=torch.int64, device=rowptr.device)
     torch.cumsum(nch, 0, out=ptr[1:])

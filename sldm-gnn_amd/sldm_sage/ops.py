@@ -199,10 +199,10 @@ def gather_rows(x: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor, num_ro
     row subset (then ``out`` holds all rows and ``edges`` is the subset's
     edge count, for the timing hook's byte accounting).  ``hub`` (a
     :class:`~sldm_sage.graph.HubPlan` of ``rowptr``): its high-degree rows
-    are summed as split edge chunks (``sldm_gather_rows_split``)."""
+    are summed as split edge chunks (``sldm_gather_rows_split``); with a row
+    subset in ``order`` the plan must list exactly the subset's hubs (rows
+    above the plan's max_deg are never summed by a row slot)."""
     dev = _require_gpu(x, rowptr, col, addend, out, order)
-    if hub is not None and order is not None:
-        raise ValueError("gather_rows: a hub plan covers all rows (no row order / subset)")
     if x.dim() != 2 or x.stride(1) != 1:
         x = x.contiguous()
     F = x.size(1)
@@ -221,7 +221,8 @@ def gather_rows(x: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor, num_ro
         with _Timed(name, bytes_alg):
             _lib.check(_lib.load().sldm_gather_rows_split(
                 dtype_code(x), x.data_ptr(), x.stride(0), rowptr.data_ptr(),
-                col.data_ptr() if E else rowptr.data_ptr(), None, num_rows, F, int(bool(mean)),
+                col.data_ptr() if E else rowptr.data_ptr(), _ptr(order), num_rows, F,
+                int(bool(mean)),
                 _ptr(addend), addend.stride(0) if addend is not None else 0,
                 dtype_code(out), out.data_ptr(), out.stride(0), hub.hub_rows.data_ptr(),
                 hub.chunk_ptr.data_ptr(), hub.num_hubs, hub.chunk_row.data_ptr(),

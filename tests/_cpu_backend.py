@@ -54,7 +54,8 @@ class CpuBackend:
         return rp, col, trp, tcol
 
     @staticmethod
-    def gather(x, rowptr, col, num_rows, mean, addend=None, rows=None, out=None, edges=None):
+    def gather(x, rowptr, col, num_rows, mean, addend=None, rows=None, out=None, edges=None,
+               hub=None):
         full = CpuBackend._gather_all(x, rowptr, col, num_rows, mean, addend)
         if rows is None:
             if out is not None:
