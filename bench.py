@@ -60,19 +60,30 @@ PMC_SUMMARY = "r2d_c4_pmc_traffic.json"   # latest committed PMC passes (tools/p
 
 
 class KernelTimer:
-    """Collects (start, end) HIP events per kernel name; durations read after sync."""
+    """Per-kernel launch durations from HIP events on the launch stream:
+    (start, end) event pairs from launches made in Python, read after a sync,
+    and milliseconds from the events the torch.ops.sldm operators record
+    around their launches in C++ (``add_ms``, via ops.flush_timing)."""
 
     def __init__(self):
         self.events: dict[str, list] = {}
+        self.ms: dict[str, list] = {}
 
     def __call__(self, name, start, end, units):
         self.events.setdefault(name, []).append((start, end, units))
 
+    def add_ms(self, name, ms, units):
+        self.ms.setdefault(name, []).append((ms, units))
+
     def summary(self):
+        from sldm_sage import ops
+        ops.flush_timing()
         out = {}
-        for name, evs in self.events.items():
-            ms = [s.elapsed_time(e) for s, e, _ in evs]
-            units = [u for _, _, u in evs]
+        for name in sorted(set(self.events) | set(self.ms)):
+            evs = self.events.get(name, [])
+            pre = self.ms.get(name, [])
+            ms = [s.elapsed_time(e) for s, e, _ in evs] + [m for m, _ in pre]
+            units = [u for _, _, u in evs] + [u for _, u in pre]
             out[name] = dict(launches=len(ms), avg_ms=sum(ms) / len(ms),
                              avg_bytes=sum(units) / len(units))
         return out
@@ -440,6 +451,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-torch-baseline", action="store_true",
                     help="skip timing the reference's ATen op sequence on the GPU")
+    ap.add_argument("--torch-baseline", action="store_true",
+                    help="time the reference's ATen op sequence on the GPU also on graphs of "
+                         "5e7 edges or more (off by default there: its [E, F] message tensors "
+                         "are 51 GB each at C4 and the leg once ended a box with a GPU memory "
+                         "fault inside torch's own index_select / scatter_add_ kernels)")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="host threads of the CPU baseline (default: every usable CPU)")
     ap.add_argument("--cpu-frac", type=int, default=10,
@@ -470,8 +486,9 @@ def main():
     t_start = time.perf_counter()
 
     def progress(msg):
-        # rank 0's progress on stderr (the JSON line stays the only stdout line)
-        if rank == 0 and use_dist:
+        # rank 0's progress on stderr before every GPU phase (the JSON line
+        # stays the only stdout line): names the phase a fault or hang is in
+        if rank == 0:
             free, total = torch.cuda.mem_get_info()
             print(f"[bench] {time.perf_counter() - t_start:7.1f} s  {msg}  [gpu free "
                   f"{free / 2**30:.0f} of {total / 2**30:.0f} GiB, peak "
@@ -587,9 +604,11 @@ def main():
                 out.backward(gout)
                 return out
 
+        progress(f"warm-up: {args.warmup} steps")
         for _ in range(args.warmup):
             blk.zero_grad(set_to_none=True)
             step()
+        barrier()
         progress("warm-up done")
         timer = KernelTimer()
         barrier()
@@ -622,6 +641,7 @@ def main():
 
         kern_all = {}
         if timed_kernels:
+            progress("per-kernel breakdown steps")
             # untimed breakdown: every op bracketed, BREAKDOWN_STEPS steps
             t_all = KernelTimer()
             ops.set_timing_hook(t_all)
@@ -635,6 +655,7 @@ def main():
         # CSR-build-inclusive step (N=1: static-graph cache cleared once)
         incl = None
         if world == 1 and not use_dist:
+            progress("CSR-inclusive step")
             graph_cache.clear()
             barrier()
             t1 = time.perf_counter()
@@ -696,7 +717,9 @@ def main():
                        gbs=round(v["avg_bytes"] / (v["avg_ms"] * 1e-3) / 1e9, 1))
                for k, v in kern.items()}
     torch_gpu = None
-    if world == 1 and not use_dist and not args.no_torch_baseline:
+    if (world == 1 and not use_dist and not args.no_torch_baseline
+            and (e < 50_000_000 or args.torch_baseline)):
+        progress("ATen op-sequence baseline on the GPU")
         ei_b, x_b = make_graph(n, e, f, dtype, dev, kind=args.graph)
         torch.manual_seed(0)
         blk_b = SageBlock([f] * (L + 1), dropout=0.25, negative_slope=0.1)
@@ -714,6 +737,7 @@ def main():
     if rank == 0:
         base = None
         if world == 1 and not args.no_cpu_baseline:
+            progress("CPU baseline (host)")
             cpus = available_cpus()
             base = cpu_baseline(cfg, args.cpu_threads or cpus["usable"], frac=args.cpu_frac)
             base["host"] = cpus

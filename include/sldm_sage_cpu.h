@@ -47,6 +47,21 @@ void sldm_cpu_post_bwd(const float* dout, const float* xhat, const float* rstd, 
                        float drop_p, uint64_t seed, int64_t row_off, float* dh, float* dgamma,
                        float* dbeta, float* dbias);
 
+/* sldm_segment_pool on the host: PyG 2.7.0 global_mean_pool / global_max_pool
+ * over the batch vector (grusage.py:3, :119-127, :185); batch [nrows] int64 in
+ * [0, num_segments).  mean_out / max_out [B, feat] (either may be NULL), empty
+ * segments give 0; max_divisor (fp32 [B, feat]) / max_first_row (int32
+ * [B, feat]) as in include/sldm_sage.h (either may be NULL). */
+void sldm_cpu_segment_pool(const float* x, int64_t ldx, const int64_t* batch, int64_t nrows,
+                           int64_t num_segments, int64_t feat, float* mean_out, int64_t ld_mean,
+                           float* max_out, int64_t ld_max, float* max_divisor,
+                           int32_t* max_first_row);
+void sldm_cpu_segment_pool_bwd(const float* x, int64_t ldx, const int64_t* batch, int64_t nrows,
+                               int64_t num_segments, int64_t feat, const float* dmean,
+                               int64_t ld_dmean, const float* max_out, int64_t ld_max,
+                               const float* dmax, int64_t ld_dmax, const float* max_divisor,
+                               const int32_t* max_first_row, float* dx, int64_t ld_dx);
+
 #ifdef __cplusplus
 }
 #endif

@@ -290,8 +290,45 @@ __device__ __forceinline__ void split_bf16x4(const float (&v)[4], uint2& hi, uin
   lo = make_uint2(pack_bf16x2(v[0] - bf16_lo(h0), v[1] - bf16_hi(h0)),
                   pack_bf16x2(v[2] - bf16_lo(h1), v[3] - bf16_hi(h1)));
 }
-// fp32 dense GEMMs on split-bf16 MFMAs (gemm.hip's NT weight-stationary
-// kernel), opt-in with SLDM_FP32_GEMM=split; default: exact fp32 MFMA.
+// Three-way split ("bf16x6" products): x = hi + mid + lo exactly (3 x 8
+// significand bits = fp32's 24); a product as the six partial products of
+// magnitude >= 2^-18 -- lo.hi + hi.lo + mid.mid + mid.hi + hi.mid + hi.hi, small
+// terms first -- on v_mfma_f32_16x16x32_bf16 with fp32 accumulation drops only
+// terms below 2^-26 relative: fp32-level products at 6 x 16 MFMA cycles per
+// 32-deep k-step against the exact fp32 MFMA's 8 x 32.
+__device__ __forceinline__ void split3_bf16x4(const float (&v)[4], uint2& hi, uint2& mid,
+                                              uint2& lo) {
+  const uint32_t h0 = pack_bf16x2(v[0], v[1]), h1 = pack_bf16x2(v[2], v[3]);
+  const float r0 = v[0] - bf16_lo(h0), r1 = v[1] - bf16_hi(h0);
+  const float r2 = v[2] - bf16_lo(h1), r3 = v[3] - bf16_hi(h1);
+  const uint32_t m0 = pack_bf16x2(r0, r1), m1 = pack_bf16x2(r2, r3);
+  hi = make_uint2(h0, h1);
+  mid = make_uint2(m0, m1);
+  lo = make_uint2(pack_bf16x2(r0 - bf16_lo(m0), r1 - bf16_hi(m0)),
+                  pack_bf16x2(r2 - bf16_lo(m1), r3 - bf16_hi(m1)));
+}
+__device__ __forceinline__ void split3_bf16x8(const float (&v)[8], bf16x8& hi, bf16x8& mid,
+                                              bf16x8& lo) {
+  const float a[4] = {v[0], v[1], v[2], v[3]}, b[4] = {v[4], v[5], v[6], v[7]};
+  uint2 h0, m0, l0, h1, m1, l1;
+  split3_bf16x4(a, h0, m0, l0);
+  split3_bf16x4(b, h1, m1, l1);
+  hi = __builtin_bit_cast(bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+  mid = __builtin_bit_cast(bf16x8, make_uint4(m0.x, m0.y, m1.x, m1.y));
+  lo = __builtin_bit_cast(bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+}
+// One accumulator update of the six-term product (operands as MFMA fragments).
+#define SLDM_MFMA_X6(acc, ah, am, al, bh, bm, bl)                                   \
+  do {                                                                              \
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);            \
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);            \
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, acc, 0, 0, 0);            \
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, acc, 0, 0, 0);            \
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, acc, 0, 0, 0);            \
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);            \
+  } while (0)
+// fp32 dense GEMMs as split-bf16 products (gemm.hip's x6 kernels; default) or
+// on the exact fp32 MFMA (SLDM_FP32_GEMM=exact).
 bool fp32_gemm_split();
 
 // Big-tile bf16 dense kernels (gemm_big.hip); the gemm.hip entry points route
@@ -329,8 +366,6 @@ int stream_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, i
                          void* out, int64_t ldo, void* out2, int64_t ldo2, hipStream_t stream);
 // gemm_ws.hip: weight-stationary dX kernel (weights in VGPRs, LDS-DMA tiles).
 bool ws_gemm_enabled();
-bool ws_fwd_enabled();
-int ws_fwd_mode();
 // gemm_tn_dma.hip: row-streaming dW kernel (LDS-DMA, transposed reads).
 bool tn_dma_enabled();
 bool tn_dma_ok(int64_t mo, int64_t n0, int64_t n1, int64_t rows, const void* a, int64_t lda,
@@ -344,15 +379,6 @@ bool ws_rowscale_ok(int64_t k, int64_t nc, int64_t num_rows, const void* a, int6
 int ws_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int64_t ldb,
                      int64_t num_rows, int64_t nc, const int32_t* rowptr, int64_t scale_cols,
                      void* out, int64_t ldo, void* out2, int64_t ldo2, hipStream_t stream);
-bool ws_dense_fwd_ok(int64_t k0, int64_t k1, int64_t nc, int64_t num_rows, const void* a0,
-                     int64_t lda0, const void* a1, int64_t lda1, const void* w, const void* out,
-                     const void* xhat);
-int ws_dense_fwd(const void* a0, int64_t lda0, int64_t k0, const void* a1, int64_t lda1,
-                 int64_t k1, const void* w, int64_t num_rows, const float* bias,
-                 const float* gamma, const float* beta, float eps, float slope, float drop_p,
-                 uint64_t seed, int64_t row_off, void* out, void* xhat, float* rstd,
-                 hipStream_t stream);
-
 }  // namespace sldm
 
 #define SLDM_REQUIRE(cond, ...)          \

@@ -26,16 +26,11 @@ namespace {
 
 constexpr int kBlock = 256;
 
-// Column partials of dgamma / dbeta / dbias: in place in LDS per row (0,
-// the default), or -- a lane's columns being fixed for every row it
-// processes -- in registers (3 NCH V floats) that meet in LDS once after the
-// row loop (1).  Same-box A/B at C4 (tools/ab.sh gpost, r2): 13.60 / 13.69 ms
-// in LDS vs 14.06 / 14.01 ms in registers: +10 VGPRs take the kernel from 4
-// to 3 waves per SIMD, and the random-row gather needs the occupancy more
-// than the LDS traffic costs.
-#ifndef SLDM_GPB_REG_PARTIALS
-#define SLDM_GPB_REG_PARTIALS 0
-#endif
+// Column partials of dgamma / dbeta / dbias accumulate in place in LDS, one
+// row of 3 F floats per row group.  (Keeping them in registers -- a lane's
+// columns are fixed -- measured slower at C4, 14.0 vs 13.6 ms: +10 VGPRs take
+// the kernel from 4 to 3 waves per SIMD, and the random-row gather needs the
+// occupancy more than the LDS traffic costs.)
 
 template <typename T, int V, int NCH, int NT>
 __global__ __launch_bounds__(kBlock) void gather_post_bwd_kernel(
@@ -75,13 +70,6 @@ __global__ __launch_bounds__(kBlock) void gather_post_bwd_kernel(
   }
   const float inv_f = 1.0f / (float)feat;
   const uint32_t dthr = sldm::dropout_threshold(drop_p);
-#if SLDM_GPB_REG_PARTIALS
-  float pgm[NCH][V], pbt[NCH][V], pbs[NCH][V];
-#pragma unroll
-  for (int c = 0; c < NCH; ++c)
-#pragma unroll
-    for (int v = 0; v < V; ++v) pgm[c][v] = pbt[c][v] = pbs[c][v] = 0.f;
-#endif
   const int64_t stride = (int64_t)gridDim.x * groups_per_block;
   const int64_t nrounds = (nrows + stride - 1) / stride;
 
@@ -187,33 +175,14 @@ __global__ __launch_bounds__(kBlock) void gather_post_bwd_kernel(
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         o[v] = rs * __builtin_fmaf(-xh[c][v], m2, gx[c][v] - m1);
-#if SLDM_GPB_REG_PARTIALS
-        pgm[c][v] = __builtin_fmaf(dy[c][v], xh[c][v], pgm[c][v]);
-        pbt[c][v] += dy[c][v];
-        pbs[c][v] += o[v];
-#else
         mine[f0[c] + v] = __builtin_fmaf(dy[c][v], xh[c][v], mine[f0[c] + v]);
         mine[feat + f0[c] + v] += dy[c][v];
         mine[2 * feat + f0[c] + v] += o[v];
-#endif
       }
       sldm::store_vec<T, V, (NT & 1) != 0>(dh + row * (int64_t)feat + f0[c], o);
     }
   }
 
-#if SLDM_GPB_REG_PARTIALS
-  // this group's partials into its LDS row (its lanes own distinct columns)
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    if (!act[c]) continue;
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      mine[f0[c] + v] = pgm[c][v];
-      mine[feat + f0[c] + v] = pbt[c][v];
-      mine[2 * feat + f0[c] + v] = pbs[c][v];
-    }
-  }
-#endif
   __syncthreads();
   for (int j = threadIdx.x; j < 3 * feat; j += kBlock) {
     float acc = 0.f;

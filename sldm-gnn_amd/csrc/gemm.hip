@@ -400,6 +400,160 @@ __global__ __launch_bounds__(kBlock, NtTile<T>::MINB) void gemm_nt_kernel(NtArgs
   nt_row_epilogue<T, MODE>(p, smem, ldc, m0, n0, BM, wave, lane);
 }
 
+// The fp32 tile kernel with split-bf16 products (fp32 in and out, fp32
+// accumulation; K a multiple of 32, 16-B aligned operands).  Each operand
+// element is split three ways, x = hi + mid + lo (bf16 each, exact), and a
+// product is the six partial products that matter (sldm::split3_bf16x4,
+// SLDM_MFMA_X6 in common.hpp): fp32-level results from six 16-cycle
+// v_mfma_f32_16x16x32_bf16 per 32-deep k-step against the exact kernel's
+// eight 32-cycle 16x16x4 fp32 MFMAs.  The A row block is split while it is
+// staged into LDS (three bf16 images); the weight fragments are split in
+// registers as they arrive from L2.  Same block / wave / epilogue structure
+// as gemm_nt_kernel<float>, on 64-row tiles (the MFMA phase no longer bounds
+// the kernel).
+template <int MT, int TPW, int MODE>
+__global__ __launch_bounds__(kBlock, 2) void gemm_nt_x6_kernel(NtArgs<float> p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int BM = 16 * MT;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q = lane >> 4, r16 = lane & 15;
+
+  int rb, cb;
+  if (p.grid_y > 1) {
+    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+    cb = j % p.grid_y;
+    rb = (j / p.grid_y) * 8 + xcd;
+  } else {
+    rb = blockIdx.x;
+    cb = 0;
+  }
+  const int64_t m0 = (int64_t)rb * BM;
+  if (m0 >= p.M) return;
+  const int n0 = cb * 16 * p.ct;
+
+  int bcol[TPW];
+  bool tval[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int tid = wave + 4 * t;
+    tval[t] = tid < p.ct;
+    int c = n0 + 16 * tid + r16;
+    bcol[t] = c < p.Nc ? c : p.Nc - 1;
+  }
+
+  f4v acc[MT][TPW];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) acc[m][t] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  // hi / mid / lo bf16 images of the staged K chunk: row pitch kce + 8
+  // elements (16 B mod 256 B per row pair: conflict-free ds_read_b128)
+  const int pa = p.kce + 8;
+  uint16_t* img_hi = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* img_mid = img_hi + BM * pa;
+  uint16_t* img_lo = img_mid + BM * pa;
+  for (int kc0 = 0; kc0 < p.K; kc0 += p.kce) {
+    if (kc0 > 0) __syncthreads();
+    constexpr int G = 8;
+    const int kc1 = min(kc0 + p.kce, p.K);
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+      const int lo = part == 0 ? kc0 : max(kc0, p.k0);
+      const int hi = part == 0 ? min(kc1, p.k0) : kc1;
+      if (lo >= hi) continue;
+      const float* base = part == 0 ? p.a0 + lo : p.a1 + (lo - p.k0);
+      const int64_t ld = part == 0 ? p.lda0 : p.lda1;
+      const int vpr = (hi - lo) / 4;
+      const int nv = BM * vpr;
+      for (int v0 = 0; v0 < nv; v0 += G * kBlock) {
+        f4v st[G];
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+          const int v = v0 + threadIdx.x + i * kBlock;
+          const int r = v / vpr;
+          const int64_t row = min(m0 + min(r, BM - 1), p.M - 1);
+          st[i] = *reinterpret_cast<const f4v*>(base + row * ld + (v - r * vpr) * 4);
+        }
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+          const int v = v0 + threadIdx.x + i * kBlock;
+          const int r = v / vpr;
+          if (v < nv) {
+            const float f[4] = {st[i][0], st[i][1], st[i][2], st[i][3]};
+            uint2 h, md, l;
+            sldm::split3_bf16x4(f, h, md, l);
+            const int off = r * pa + (lo - kc0) + (v - r * vpr) * 4;
+            *reinterpret_cast<uint2*>(img_hi + off) = h;
+            *reinterpret_cast<uint2*>(img_mid + off) = md;
+            *reinterpret_cast<uint2*>(img_lo + off) = l;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const int kend = kc1 - kc0;                         // a multiple of 32
+    // weight fragments: 8 consecutive k of column bcol[t] per lane, fetched
+    // one k-step ahead (two register sets), split on use
+    f4v bx[TPW][2], by[TPW][2];
+    auto loadb = [&](f4v (&bb)[TPW][2], int k) {
+      const int ks = min(k, kend - 32);
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        const float* src = p.b + (int64_t)bcol[t] * p.ldb + kc0 + ks + 8 * q;
+        bb[t][0] = *reinterpret_cast<const f4v*>(src);
+        bb[t][1] = *reinterpret_cast<const f4v*>(src + 4);
+      }
+    };
+    auto mma = [&](f4v (&bb)[TPW][2], int k) {
+      if (k >= kend) return;
+      s8v ahi[MT], amid[MT], alo[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int off = (16 * m + r16) * pa + k + 8 * q;
+        ahi[m] = *reinterpret_cast<const s8v*>(img_hi + off);
+        amid[m] = *reinterpret_cast<const s8v*>(img_mid + off);
+        alo[m] = *reinterpret_cast<const s8v*>(img_lo + off);
+      }
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        if (!tval[t]) continue;
+        const float w[8] = {bb[t][0][0], bb[t][0][1], bb[t][0][2], bb[t][0][3],
+                            bb[t][1][0], bb[t][1][1], bb[t][1][2], bb[t][1][3]};
+        s8v whi, wmid, wlo;
+        sldm::split3_bf16x8(w, whi, wmid, wlo);
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          SLDM_MFMA_X6(acc[m][t], ahi[m], amid[m], alo[m], whi, wmid, wlo);
+      }
+    };
+    loadb(bx, 0);
+    for (int k0 = 0; k0 < kend; k0 += 64) {
+      loadb(by, k0 + 32);
+      mma(bx, k0);
+      if (k0 + 32 >= kend) break;
+      loadb(bx, k0 + 64);
+      mma(by, k0 + 32);
+    }
+  }
+  __syncthreads();  // LDS now holds the C tile
+
+  const int ldc = 16 * p.ct + 4;
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    if (!tval[t]) continue;
+    const int c = 16 * (wave + 4 * t) + r16;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) smem[(16 * m + 4 * q + r) * ldc + c] = acc[m][t][r];
+  }
+  __syncthreads();
+
+  nt_row_epilogue<float, MODE>(p, smem, ldc, m0, n0, BM, wave, lane);
+}
+
 // fp32 weight-stationary NT (exact-fp32 LN forward and dX with one column
 // block, Nc <= 256, K = KC in {128, 256}; C2's shapes).  The tile kernel above
 // re-reads its weight fragments from L2 every k-step and stages each A tile
@@ -504,129 +658,6 @@ __global__ __launch_bounds__(kBlock, 2) void gemm_nt_ws32_kernel(NtArgs<float> p
   }
 }
 
-// The same weight-stationary NT kernel with split-bf16 products (fp32 in and
-// out, fp32 accumulation): the weights are split once into hi / lo bf16
-// B-fragments (32-deep k-steps: the same VGPR count as the fp32 fragments), A
-// tiles are split while they are staged into LDS (hi and lo bf16 images), and
-// each 32-deep k-step is three v_mfma_f32_16x16x32_bf16 (lo·hi, hi·lo, hi·hi)
-// where the exact kernel issues eight 16x16x4 fp32 MFMAs of twice the cycles.
-// ~2^-16 relative per product; the epilogue is the exact kernel's.
-template <int TPW, int KC, int MODE>
-__global__ __launch_bounds__(kBlock, 2) void gemm_nt_ws32x3_kernel(NtArgs<float> p,
-                                                                    int64_t ntiles) {
-  constexpr int MT = 2, BM = 32;
-  constexpr int KS3 = KC / 32;              // 32-deep k-steps
-  constexpr int VPR = KC / 4;               // 16-B fp32 vectors per A row
-  constexpr int NV = BM * VPR / kBlock;
-  constexpr int PB = 2 * KC + 16;           // bf16 image row pitch (bytes)
-  static_assert(BM * VPR % kBlock == 0 && KC % 32 == 0, "ws32x3 shape");
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  char* img_hi = reinterpret_cast<char*>(smem);
-  char* img_lo = img_hi + BM * PB;
-  float* lds_c = reinterpret_cast<float*>(img_lo + BM * PB);
-  const int ldc = 16 * p.ct + 4;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int q = lane >> 4, r16 = lane & 15;
-
-  int64_t tile = blockIdx.x;
-  if (tile >= ntiles) return;
-
-  bool tval[TPW];
-  s8v whi[KS3][TPW], wlo[KS3][TPW];
-#pragma unroll
-  for (int t = 0; t < TPW; ++t) {
-    const int tid = wave + 4 * t;
-    tval[t] = tid < p.ct;
-    const int c = 16 * tid + r16;
-    const int bc = c < p.Nc ? c : p.Nc - 1;
-#pragma unroll
-    for (int ks = 0; ks < KS3; ++ks) {
-      const f4v u0 = nt_load_b<float, true>(p, bc, 32 * ks + 8 * q);
-      const f4v u1 = nt_load_b<float, true>(p, bc, 32 * ks + 8 * q + 4);
-      const float v[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
-      sldm::split_bf16x8(v, whi[ks][t], wlo[ks][t]);
-    }
-  }
-
-  f4v st[NV];
-  auto load_tile = [&](int64_t tl) {
-    const int64_t m0 = tl * BM;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int v = threadIdx.x + i * kBlock;
-      const int r = v / VPR, kv = (v - r * VPR) * 4;
-      const int64_t row = min(m0 + r, p.M - 1);
-      const float* src = kv < p.k0 ? p.a0 + row * p.lda0 + kv : p.a1 + row * p.lda1 + (kv - p.k0);
-      st[i] = *reinterpret_cast<const f4v*>(src);
-    }
-  };
-  load_tile(tile);
-  for (; tile < ntiles; tile += gridDim.x) {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int v = threadIdx.x + i * kBlock;
-      const int r = v / VPR, kv = (v - r * VPR) * 4;
-      const float f[4] = {st[i][0], st[i][1], st[i][2], st[i][3]};
-      uint2 h, l;
-      sldm::split_bf16x4(f, h, l);
-      *reinterpret_cast<uint2*>(img_hi + r * PB + 2 * kv) = h;
-      *reinterpret_cast<uint2*>(img_lo + r * PB + 2 * kv) = l;
-    }
-    __syncthreads();
-    if (tile + gridDim.x < ntiles) load_tile(tile + gridDim.x);
-
-    f4v acc[MT][TPW];
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int t = 0; t < TPW; ++t) acc[m][t] = f4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < KS3; ++ks) {
-      s8v ahi[MT], alo[MT];
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const int off = (16 * m + r16) * PB + 64 * ks + 16 * q;
-        ahi[m] = *reinterpret_cast<const s8v*>(img_hi + off);
-        alo[m] = *reinterpret_cast<const s8v*>(img_lo + off);
-      }
-#pragma unroll
-      for (int t = 0; t < TPW; ++t) {
-        if (!tval[t]) continue;
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[m], whi[ks][t], acc[m][t], 0, 0, 0);
-          acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[m], wlo[ks][t], acc[m][t], 0, 0, 0);
-          acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[m], whi[ks][t], acc[m][t], 0, 0, 0);
-        }
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-      if (!tval[t]) continue;
-      const int c = 16 * (wave + 4 * t) + r16;
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) lds_c[(16 * m + 4 * q + r) * ldc + c] = acc[m][t][r];
-    }
-    __syncthreads();
-    nt_row_epilogue<float, MODE>(p, lds_c, ldc, tile * BM, 0, BM, wave, lane);
-  }
-}
-
-template <int TP, int KCV, int MODE>
-int launch_ws32x3_t(const NtArgs<float>& p, int64_t ntiles, int64_t grid, hipStream_t stream) {
-  const size_t lds = (size_t)2 * 32 * (2 * KCV + 16) + sizeof(float) * 32 * (size_t)(16 * p.ct + 4);
-  auto kern = gemm_nt_ws32x3_kernel<TP, KCV, MODE>;
-  if (lds > 65536)
-    SLDM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  kern<<<(unsigned)grid, kBlock, lds, stream>>>(p, ntiles);
-  SLDM_LAUNCH_CHECK("gemm_nt_ws32x3_kernel");
-  return SLDM_OK;
-}
-
 template <int TP, int KCV, int MODE>
 int launch_ws32_t(const NtArgs<float>& p, int64_t ntiles, int64_t grid, size_t lds,
                   hipStream_t stream) {
@@ -651,14 +682,6 @@ int launch_nt_ws32(const NtArgs<float>& p, int tpw, hipStream_t stream) {
     return -1;
   const int64_t ntiles = (p.M + 31) / 32;
   const int64_t grid = ntiles < 512 ? ntiles : 512;   // 2 blocks x 256 CUs, persistent
-  if (sldm::fp32_gemm_split()) {
-    if (p.K == 256 && tpw == 1) return launch_ws32x3_t<1, 256, MODE>(p, ntiles, grid, stream);
-    if (p.K == 256 && tpw == 2) return launch_ws32x3_t<2, 256, MODE>(p, ntiles, grid, stream);
-    if (p.K == 128 && tpw == 1) return launch_ws32x3_t<1, 128, MODE>(p, ntiles, grid, stream);
-    if (p.K == 128 && tpw == 2) return launch_ws32x3_t<2, 128, MODE>(p, ntiles, grid, stream);
-    if (p.K == 128 && tpw == 3) return launch_ws32x3_t<3, 128, MODE>(p, ntiles, grid, stream);
-    if (p.K == 128 && tpw == 4) return launch_ws32x3_t<4, 128, MODE>(p, ntiles, grid, stream);
-  }
   const size_t lds = sizeof(float) * (32 * (size_t)(p.K + 4) + 32 * (size_t)(16 * p.ct + 4));
   if (p.K == 256 && tpw == 1) return launch_ws32_t<1, 256, MODE>(p, ntiles, grid, lds, stream);
   if (p.K == 256 && tpw == 2) return launch_ws32_t<2, 256, MODE>(p, ntiles, grid, lds, stream);
@@ -689,6 +712,25 @@ int launch_nt_t(const NtArgs<T>& p, hipStream_t stream) {
   return SLDM_OK;
 }
 
+template <int TPW, int MODE>
+int launch_nt_x6_t(const NtArgs<float>& p, hipStream_t stream) {
+  constexpr int MT = 4, BM = 16 * MT;
+  int64_t nrb = (p.M + BM - 1) / BM;
+  if (p.grid_y > 1) nrb = (nrb + 7) / 8 * 8;
+  const int64_t grid = nrb * p.grid_y;
+  SLDM_REQUIRE(grid < ((int64_t)1 << 31), "gemm_nt: grid too large");
+  const size_t lds_c = sizeof(float) * (size_t)BM * (size_t)(16 * p.ct + 4);
+  const size_t lds_a = 3 * sizeof(uint16_t) * (size_t)BM * (size_t)(p.kce + 8);
+  const size_t lds = lds_c > lds_a ? lds_c : lds_a;
+  auto kern = gemm_nt_x6_kernel<MT, TPW, MODE>;
+  if (lds > 65536)
+    SLDM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  kern<<<(unsigned)grid, kBlock, lds, stream>>>(p);
+  SLDM_LAUNCH_CHECK("gemm_nt_x6_kernel");
+  return SLDM_OK;
+}
+
 template <typename T, int MODE>
 int launch_nt(NtArgs<T>& p, hipStream_t stream) {
   constexpr int EPL = NtOps<T>::EPL;
@@ -713,6 +755,20 @@ int launch_nt(NtArgs<T>& p, hipStream_t stream) {
                    (k1 == 0 || al(p.a1)) && al(p.b) && (p.K % KS == 0);
   const int tpw = (p.ct + 3) / 4;
   if constexpr (sizeof(T) == 4) {
+    // split-bf16 products for the vector shapes (K a multiple of 32)
+    if (vec && p.K % 32 == 0 && p.kce % 32 == 0 && sldm::fp32_gemm_split()) {
+      // 128-deep K chunks: the three staged images stay below the C tile's
+      // LDS footprint (two blocks per CU)
+      NtArgs<float> q = p;
+      q.kce = p.kce < 128 ? p.kce : 128;
+      switch (tpw) {
+        case 1: return launch_nt_x6_t<1, MODE>(q, stream);
+        case 2: return launch_nt_x6_t<2, MODE>(q, stream);
+        case 3: return launch_nt_x6_t<3, MODE>(q, stream);
+        case 4: return launch_nt_x6_t<4, MODE>(q, stream);
+      }
+    }
+    // exact fp32 MFMA: the weight-stationary kernel where its shape fits
     const int rc = launch_nt_ws32<MODE>(p, tpw, stream);
     if (rc >= 0) return rc;
   }
@@ -916,6 +972,125 @@ __global__ __launch_bounds__(kBlock) void gemm_tn_kernel(TnArgs<T> p) {
     }
 }
 
+// The fp32 TN kernel with split-bf16 products (see gemm_nt_x6_kernel): both
+// staged operand tiles become hi / mid / lo bf16 images in LDS as they are
+// stored, and the MFMA phase is the bf16 kernel's transposed reads with the
+// six-term product per accumulator and 32-row k-step instead of eight exact
+// 16x16x4 fp32 MFMAs.  16-B aligned operands.
+__global__ __launch_bounds__(kBlock) void gemm_tn_x6_kernel(TnArgs<float> p) {
+  constexpr int PITCH = TnLds<uint16_t>::pitch;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[6 * TN_BK * PITCH];
+  uint16_t* a_hi = lds;
+  uint16_t* a_mid = lds + TN_BK * PITCH;
+  uint16_t* a_lo = lds + 2 * TN_BK * PITCH;
+  uint16_t* b_hi = lds + 3 * TN_BK * PITCH;
+  uint16_t* b_mid = lds + 4 * TN_BK * PITCH;
+  uint16_t* b_lo = lds + 5 * TN_BK * PITCH;
+
+  const int b = blockIdx.x;
+  const int tiles = p.tiles_m * p.tiles_n;
+  int split, tile;
+  if (p.splits % 8 == 0) {
+    const int xcd = b % 8, j = b / 8;
+    tile = j % tiles;
+    split = (j / tiles) * 8 + xcd;
+  } else {
+    tile = b % tiles;
+    split = b / tiles;
+  }
+  const int tm = tile / p.tiles_n, tn = tile % p.tiles_n;
+  const int mbase = tm * TN_TILE, nbase = tn * TN_TILE;
+  const int64_t kbeg = (int64_t)split * p.chunk;
+  const int64_t kend = min(kbeg + p.chunk, p.rows);
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane >> 4, r16 = lane & 15;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  f4v acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  auto elem_a = [&](int64_t k, int c) { return p.a + k * p.lda + c; };
+  auto elem_b = [&](int64_t k, int c) {
+    return c < p.n0 ? p.b0 + k * p.ldb0 + c : p.b1 + k * p.ldb1 + (c - p.n0);
+  };
+  using Stage = TnStage<float, true>;
+  auto store_split = [&](const Stage& st, uint16_t* hi, uint16_t* mid, uint16_t* lo) {
+#pragma unroll
+    for (int i = 0; i < Stage::NV; ++i) {
+      const int idx = threadIdx.x + i * kBlock;
+      const int r = idx / (TN_TILE / 4);
+      const int cv = (idx % (TN_TILE / 4)) * 4;
+      const float f[4] = {__uint_as_float(st.v[i].x), __uint_as_float(st.v[i].y),
+                          __uint_as_float(st.v[i].z), __uint_as_float(st.v[i].w)};
+      uint2 h, md, l;
+      sldm::split3_bf16x4(f, h, md, l);
+      *reinterpret_cast<uint2*>(hi + r * PITCH + cv) = h;
+      *reinterpret_cast<uint2*>(mid + r * PITCH + cv) = md;
+      *reinterpret_cast<uint2*>(lo + r * PITCH + cv) = l;
+    }
+  };
+  auto read_tr = [&](const uint16_t* img, int rr, int col) {
+    const uint16_t* pa = img + rr * PITCH + col;
+    const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s4v*)(pa));
+    const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s4v*)(pa + 4 * PITCH));
+    return s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  Stage sa, sb;
+  if (kbeg < kend) {
+    sa.load(elem_a, kbeg, mbase, kend, p.mo);
+    sb.load(elem_b, kbeg, nbase, kend, p.nn);
+  }
+  for (int64_t k0 = kbeg; k0 < kend; k0 += TN_BK) {
+    __syncthreads();
+    store_split(sa, a_hi, a_mid, a_lo);
+    store_split(sb, b_hi, b_mid, b_lo);
+    __syncthreads();
+    if (k0 + TN_BK < kend) {
+      sa.load(elem_a, k0 + TN_BK, mbase, kend, p.mo);
+      sb.load(elem_b, k0 + TN_BK, nbase, kend, p.nn);
+    }
+#pragma unroll
+    for (int kb = 0; kb < TN_BK; kb += 32) {
+      const int rr = kb + 8 * q + (r16 >> 2);
+      const int cc = 4 * (r16 & 3);
+      s8v ah[4], am[4], al[4], bh[4], bm[4], bl[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ah[i] = read_tr(a_hi, rr, wm * 64 + 16 * i + cc);
+        am[i] = read_tr(a_mid, rr, wm * 64 + 16 * i + cc);
+        al[i] = read_tr(a_lo, rr, wm * 64 + 16 * i + cc);
+        bh[i] = read_tr(b_hi, rr, wn * 64 + 16 * i + cc);
+        bm[i] = read_tr(b_mid, rr, wn * 64 + 16 * i + cc);
+        bl[i] = read_tr(b_lo, rr, wn * 64 + 16 * i + cc);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          SLDM_MFMA_X6(acc[i][j], ah[i], am[i], al[i], bh[j], bm[j], bl[j]);
+    }
+  }
+
+  float* out = p.slab + (int64_t)split * p.mo * p.nn;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = nbase + wn * 64 + 16 * j + r16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mbase + wm * 64 + 16 * i + 4 * q + r;
+        if (row < p.mo && col < p.nn) out[(int64_t)row * p.nn + col] = acc[i][j][r];
+      }
+    }
+}
+
 // out1 != nullptr: element (row, col) of the [mo, nn] result goes to out
 // [mo, n0] for col < n0 and to out1 [mo, nn - n0] otherwise (dW_l, dW_r).
 __global__ __launch_bounds__(kBlock) void slab_reduce_kernel(const float* __restrict__ slab,
@@ -1008,10 +1183,6 @@ extern "C" int sldm_sage_dense_fwd(int dtype, const void* a0, int64_t lda0, int6
   SLDM_REQUIRE(a0 && w && out && gamma && beta && (k1 == 0 || a1),
                "sldm_sage_dense_fwd: NULL argument");
   hipStream_t stream = sldm::as_stream(stream_);
-  if (dtype == SLDM_BF16 && sldm::ws_fwd_enabled() &&
-      sldm::ws_dense_fwd_ok(k0, k1, nc, num_rows, a0, lda0, a1, lda1, w, out, xhat))
-    return sldm::ws_dense_fwd(a0, lda0, k0, a1, lda1, k1, w, num_rows, bias, gamma, beta, eps,
-                              negative_slope, drop_p, seed, row_off, out, xhat, rstd, stream);
   if (dtype == SLDM_BF16 && sldm::stream_gemm_enabled() &&
       sldm::stream_dense_fwd_ok(k0, k0 + k1, nc, a0, lda0, k1 ? a1 : a0, k1 ? lda1 : lda0, w,
                                 out, xhat, negative_slope))
@@ -1153,7 +1324,15 @@ int gemm_tn_impl(int dtype, const void* a, int64_t lda, int64_t mo, const void* 
                      (ldb0 % EPV == 0) && (n1 == 0 || ldb1 % EPV == 0) && al(a) && al(b0) &&
                      (n1 == 0 || al(b1));
     const unsigned grid = (unsigned)(pl.splits * pl.tiles_m * pl.tiles_n);
-    if (vec)
+    bool x6 = false;
+    if constexpr (sizeof(T) == 4) {
+      if (vec && sldm::fp32_gemm_split()) {
+        gemm_tn_x6_kernel<<<grid, kBlock, 0, stream>>>(p);
+        x6 = true;
+      }
+    }
+    if (x6) {
+    } else if (vec)
       gemm_tn_kernel<T, true><<<grid, kBlock, 0, stream>>>(p);
     else
       gemm_tn_kernel<T, false><<<grid, kBlock, 0, stream>>>(p);
@@ -1186,12 +1365,13 @@ extern "C" int sldm_gemm_tn_split(int dtype, const void* a, int64_t lda, int64_t
 }
 
 namespace sldm {
-// Opt-in (SLDM_FP32_GEMM=split): the split form is ~2^-16 relative per
-// product, which flips LeakyReLU branches of pre-activations within ~1e-5 of
-// zero against the fp32 oracle; the exact kernels (~1e-7) stay the default.
-// Read per call so tests can compare both forms in one process.
+// fp32 dense GEMMs run as split-bf16 products (hi.hi + hi.lo + lo.hi on the
+// bf16 MFMA, ~2^-16 relative per product, fp32 accumulation) wherever a
+// kernel has that form; SLDM_FP32_GEMM=exact selects the exact fp32 MFMA
+// (v_mfma_f32_16x16x4_f32, 1/16 of the bf16 rate) everywhere.  Read per call
+// so tests can compare both forms in one process.
 bool fp32_gemm_split() {
   const char* e = getenv("SLDM_FP32_GEMM");
-  return e && e[0] == 's';
+  return !(e && e[0] == 'e');
 }
 }  // namespace sldm

@@ -230,191 +230,6 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
   }
 }
 
-// ---- LN / act / dropout backward, operand rows streamed through LDS ------
-// The same per-element math as post_bwd_kernel (dh bit-identical) for rows of
-// 512 B (bf16 F = 256, fp32 F = 128: 32 lanes x 16 B, two rows per wave), with
-// the two streamed operands (dout, xhat) fetched HBM -> LDS by LDS-DMA
-// (global_load_lds_dwordx4) into a per-wave ring of kRingStages row pairs.
-// The register kernel keeps its loads in VGPRs, so the bytes it has in flight
-// are bounded by its registers (two rows per row group; four took it from 4 to
-// 3 waves per SIMD and ran slower); here S - 1 row pairs per wave are in
-// flight whatever the compute holds.  Waves own their ring slots, so there is
-// no block barrier in the loop: one counted s_waitcnt vmcnt per row pair.
-//
-// vmcnt bookkeeping (every vector-memory op of the loop is asm the compiler
-// does not see): iteration k stores dh(k) [1 op] then issues the loads of row
-// pair k + S - 1 [dout DMA, xhat DMA, rstd: 3 ops]; the prologue issues the
-// loads of pairs 0 .. S-2.  The loads of pair m are followed by 4 (S - 2)
-// younger ops in the steady state and by 3 (S - 2) + m in the first S - 1
-// iterations.  Row pairs past a wave's last one are re-loads of that last
-// pair (harmless dummies keep the count); the final pair of an odd row count
-// reads its single row into both halves, whose identical results go to the
-// same row (the second half adds nothing to the column partials).
-constexpr int kRingStages = 8;
-
-__device__ __forceinline__ void ring_dma16(const void* sbase, uint32_t voff, uint32_t lds_addr) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
-               :: "v"(voff), "s"(sbase), "s"(lds_addr) : "memory", "m0");
-}
-__device__ __forceinline__ float ring_load_f32(const void* sbase, uint32_t voff) {
-  float r;
-  asm volatile("global_load_dword %0, %1, %2" : "=v"(r) : "v"(voff), "s"(sbase) : "memory");
-  return r;
-}
-__device__ __forceinline__ void ring_store16(void* sbase, uint32_t voff, sldm::u32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, %2" :: "v"(voff), "v"(v), "s"(sbase) : "memory");
-}
-// Waits until at most N vector-memory ops are outstanding; tying the rstd
-// register of the pair it releases to the wait keeps its uses after it.
-template <int N>
-__device__ __forceinline__ void ring_wait(float& r) {
-  asm volatile("s_waitcnt vmcnt(%1)" : "+v"(r) : "n"(N) : "memory");
-}
-
-template <int I, int N, typename Fn>
-__device__ __forceinline__ void ring_static_for_(Fn&& fn) {
-  if constexpr (I < N) {
-    fn(std::integral_constant<int, I>{});
-    ring_static_for_<I + 1, N>(fn);
-  }
-}
-template <int N, typename Fn>
-__device__ __forceinline__ void ring_static_for(Fn&& fn) { ring_static_for_<0, N>(fn); }
-
-template <typename T>
-__global__ __launch_bounds__(kBlock) void post_bwd_ring_kernel(
-    const T* __restrict__ dout, const T* __restrict__ xhat, const float* __restrict__ rstd,
-    int64_t nrows, const float* __restrict__ gamma, const float* __restrict__ beta, float slope,
-    float drop_p, float drop_scale, uint64_t seed, int64_t row_off, T* __restrict__ dh,
-    float* __restrict__ partials) {
-#pragma clang fp contract(off)
-  constexpr int V = 16 / (int)sizeof(T);
-  constexpr int F = 32 * V;                    // 512-B rows
-  constexpr int S = kRingStages;
-  constexpr int WAVES = kBlock / 64;
-  constexpr uint32_t SLOT = 2 * 2 * 512;       // dout pair + xhat pair
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int half = lane >> 5;                  // row of the pair
-  const int f0 = (lane & 31) * V;
-
-  float gm[V], bt[V], pg[V], pb[V], pd[V];
-#pragma unroll
-  for (int k = 0; k < V; ++k) {
-    gm[k] = gamma[f0 + k];
-    bt[k] = beta[f0 + k];
-    pg[k] = pb[k] = pd[k] = 0.0f;
-  }
-  // consume gamma / beta before the ring starts: the compiler's own wait for
-  // these loads lands here, not inside the loop (where it would be a vmcnt(0)
-  // draining the ring once per pass)
-#pragma unroll
-  for (int k = 0; k < V; ++k) asm volatile("" : "+v"(gm[k]), "+v"(bt[k]));
-  const float inv_f = 1.0f / (float)F;
-  const uint32_t dthr = sldm::dropout_threshold(drop_p);
-
-  const int64_t npairs = (nrows + 1) >> 1;
-  const int64_t gw = (int64_t)blockIdx.x * WAVES + wave;
-  const int64_t nw = (int64_t)gridDim.x * WAVES;
-  const int64_t njobs = gw < npairs ? (npairs - 1 - gw) / nw + 1 : 0;
-  const uint32_t lds_w =
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)smem + wave * S * SLOT;
-  const char* ring = smem + wave * S * SLOT;
-
-  float rsr[S];
-  auto pair_of = [&](int64_t job) { return gw + (job < njobs ? job : njobs - 1) * nw; };
-  auto issue = [&](int64_t job, int slot) {
-    const int64_t pr = pair_of(job);
-    const uint32_t lrow = (2 * pr + 1 >= nrows) ? 0u : (uint32_t)half;
-    const uint32_t voff = (lrow * 32 + (uint32_t)(lane & 31)) * 16;
-    ring_dma16(dout + 2 * pr * F, voff, lds_w + slot * SLOT);
-    ring_dma16(xhat + 2 * pr * F, voff, lds_w + slot * SLOT + 1024);
-    rsr[slot] = ring_load_f32(rstd + 2 * pr, lrow * 4);
-  };
-
-  if (njobs > 0) {
-#pragma unroll
-    for (int s = 0; s < S - 1; ++s) issue(s, s);
-  }
-  for (int64_t j0 = 0; j0 < njobs; j0 += S) {
-    // stage s as a compile-time constant (ring slot, rstd register, counts)
-    ring_static_for<S>([&](auto sc) {
-      constexpr int s = decltype(sc)::value;
-      const int64_t job = j0 + s;
-      if (job >= njobs) return;
-      if (j0 == 0 && s < S - 1) ring_wait<3 * (S - 2) + (s < S - 2 ? s : S - 2)>(rsr[s]);
-      else ring_wait<4 * (S - 2)>(rsr[s]);
-      const int64_t pr = gw + job * nw;
-      const bool tail = 2 * pr + 1 >= nrows;
-      const bool live = !tail || half == 0;
-      const int64_t row = 2 * pr + (tail ? 0 : half);
-      float go[V], xh[V];
-      sldm::Vec<T, V>::load(reinterpret_cast<const T*>(ring + s * SLOT + lane * 16), go);
-      sldm::Vec<T, V>::load(reinterpret_cast<const T*>(ring + s * SLOT + 1024 + lane * 16), xh);
-      const float rs = rsr[s];
-      const uint32_t rkey = sldm::dropout_row_key(seed, (uint64_t)(row + row_off));
-      bool kp[V];
-#pragma unroll
-      for (int k = 0; k < V; ++k) kp[k] = true;
-      if (drop_p > 0.0f) sldm::dropout_keepv<V>(rkey, (uint32_t)f0, dthr, kp);
-      float gx[V], dy[V];
-      float s1 = 0.0f, s2 = 0.0f;
-#pragma unroll
-      for (int k = 0; k < V; ++k) {
-        const float g = gm[k];
-        float d = kp[k] ? go[k] * drop_scale : 0.0f;
-        const bool pos = __builtin_fmaf(xh[k], g, bt[k]) > 0.0f;
-        d = pos ? d : d * slope;
-        dy[k] = d;
-        gx[k] = d * g;
-        s1 += gx[k];
-        s2 = __builtin_fmaf(gx[k], xh[k], s2);
-      }
-      const float m1 = group_sum(s1, 32) * inv_f;
-      const float m2 = group_sum(s2, 32) * inv_f;
-      float o[V];
-#pragma unroll
-      for (int k = 0; k < V; ++k) {
-        o[k] = rs * __builtin_fmaf(-xh[k], m2, gx[k] - m1);
-        pg[k] = live ? __builtin_fmaf(dy[k], xh[k], pg[k]) : pg[k];
-        pb[k] = live ? pb[k] + dy[k] : pb[k];
-        pd[k] = live ? pd[k] + o[k] : pd[k];
-      }
-      sldm::u32x4 w;
-      if constexpr (sizeof(T) == 2) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w[i] = sldm::pack_bf16x2(o[2 * i], o[2 * i + 1]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w[i] = __float_as_uint(o[i]);
-      }
-      const uint32_t lrow = tail ? 0u : (uint32_t)half;
-      ring_store16(dh + 2 * pr * F, (lrow * 32 + (uint32_t)(lane & 31)) * 16, w);
-      issue(job + S - 1, (s + S - 1) % S);
-    });
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA in flight into the reused LDS
-  __syncthreads();
-
-  // Block reduction of the column partials: 2 * WAVES row groups of [3][F],
-  // summed in group order.
-  float* red = reinterpret_cast<float*>(smem);
-  float* mine = red + (size_t)(wave * 2 + half) * 3 * F;
-#pragma unroll
-  for (int k = 0; k < V; ++k) {
-    mine[f0 + k] = pg[k];
-    mine[F + f0 + k] = pb[k];
-    mine[2 * F + f0 + k] = pd[k];
-  }
-  __syncthreads();
-  for (int j = threadIdx.x; j < 3 * F; j += kBlock) {
-    float acc = 0.0f;
-    for (int g = 0; g < 2 * WAVES; ++g) acc += red[(size_t)g * 3 * F + j];
-    partials[(size_t)blockIdx.x * 3 * F + j] = acc;
-  }
-}
-
 // out[j] = sum_p partials[p][j]: a block owns 32 columns; its 8 row groups sum
 // the partials p == g (mod 8) (4 loads in flight each), then one thread adds
 // the 8 group sums in order: fixed order, deterministic.
@@ -562,16 +377,6 @@ int post_bwd_t(const RowGeom& g, const void* dout, const void* xhat, const void*
   return SLDM_ERR_ARG;
 }
 
-bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
-
-// Opt-in (SLDM_POST_RING=1): measured 3.37-3.39 ms against the register
-// kernel's 3.30-3.31 ms at C4 (same box), so bytes in flight were not what
-// held the register kernel at ~4.6 TB/s.
-bool post_ring_enabled() {
-  const char* e = getenv("SLDM_POST_RING");
-  return e && e[0] == '1';
-}
-
 }  // namespace
 
 extern "C" int sldm_post_fwd(int h_dtype, const void* h, int64_t ldh, int64_t num_rows,
@@ -629,23 +434,6 @@ extern "C" int sldm_post_bwd(int dtype, const void* dout, const void* xhat, cons
   hipStream_t stream = sldm::as_stream(stream_);
   const int f = (int)feat;
   int eb = (dtype == SLDM_F32 || dh_dtype == SLDM_F32) ? 4 : 2;
-  // 512-B rows, no saved-output branch, dh in the input dtype: the LDS-ring
-  // kernel when SLDM_POST_RING=1
-  if (!zout && dtype == dh_dtype && feat * eb == 512 && post_ring_enabled() &&
-      aligned16(dout) && aligned16(xhat) && aligned16(dh)) {
-    // (zero rows: every wave has no pair and the partials are written as 0)
-    const size_t lds = (size_t)kRingStages * 2048 * (kBlock / 64);
-    if (dtype == SLDM_BF16)
-      post_bwd_ring_kernel<uint16_t><<<num_partials, kBlock, lds, stream>>>(
-          (const uint16_t*)dout, (const uint16_t*)xhat, rstd, num_rows, gamma, beta,
-          negative_slope, drop_p, scale, seed, row_off, (uint16_t*)dh, col_partials);
-    else
-      post_bwd_ring_kernel<float><<<num_partials, kBlock, lds, stream>>>(
-          (const float*)dout, (const float*)xhat, rstd, num_rows, gamma, beta, negative_slope,
-          drop_p, scale, seed, row_off, (float*)dh, col_partials);
-    SLDM_LAUNCH_CHECK("post_bwd_ring_kernel");
-    return SLDM_OK;
-  }
   RowGeom g = row_geom(eb, feat, {dout, xhat, dh});
   if (dtype == SLDM_F32 && dh_dtype == SLDM_F32)
     return post_bwd_t<float, float>(g, dout, xhat, zout, rstd, num_rows, f, gamma, beta, negative_slope, drop_p, scale, seed, row_off, dh, col_partials, num_partials, stream);

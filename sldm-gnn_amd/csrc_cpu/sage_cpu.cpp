@@ -198,6 +198,81 @@ void sldm_cpu_post_bwd(const float* dout, const float* xhat, const float* rstd, 
   }
 }
 
-int sldm_cpu_abi_version(void) { return 1; }
+// Graph-level readout on the host (grusage.py:119-127, :185): PyG 2.7.0
+// global_mean_pool / global_max_pool = utils.scatter(x, batch, reduce) at
+// dim_size B.  Rows are visited in order, so a segment's fp32 sum is the
+// reference's scatter_add_ order; OpenMP over columns.
+void sldm_cpu_segment_pool(const float* x, int64_t ldx, const int64_t* batch, int64_t nrows,
+                           int64_t num_segments, int64_t feat, float* mean_out, int64_t ld_mean,
+                           float* max_out, int64_t ld_max, float* max_divisor,
+                           int32_t* max_first_row) {
+  const int64_t B = num_segments;
+  std::vector<int64_t> count((size_t)B, 0);
+  for (int64_t i = 0; i < nrows; ++i) ++count[(size_t)batch[i]];
+#pragma omp parallel for schedule(static)
+  for (int64_t f = 0; f < feat; ++f) {
+    if (mean_out) {
+      for (int64_t b = 0; b < B; ++b) mean_out[b * ld_mean + f] = 0.f;
+      for (int64_t i = 0; i < nrows; ++i) mean_out[batch[i] * ld_mean + f] += x[i * ldx + f];
+      for (int64_t b = 0; b < B; ++b)
+        mean_out[b * ld_mean + f] /= (float)(count[(size_t)b] > 0 ? count[(size_t)b] : 1);
+    }
+    if (max_out) {
+      std::vector<char> seen((size_t)B, 0);
+      std::vector<int32_t> ties((size_t)B, 0), first((size_t)B, 0);
+      for (int64_t b = 0; b < B; ++b) max_out[b * ld_max + f] = 0.f;   // empty segments
+      for (int64_t i = 0; i < nrows; ++i) {
+        const int64_t b = batch[i];
+        const float v = x[i * ldx + f];
+        float& m = max_out[b * ld_max + f];
+        if (!seen[(size_t)b] || v > m) {
+          m = v;
+          seen[(size_t)b] = 1;
+          ties[(size_t)b] = 1;
+          first[(size_t)b] = (int32_t)i;
+        } else if (v == m) {
+          ++ties[(size_t)b];
+        }
+      }
+      for (int64_t b = 0; b < B; ++b) {
+        // torch's amax backward divides by the entries equal to the result,
+        // the zero-initialised output included when the result is 0
+        if (max_divisor)
+          max_divisor[b * feat + f] =
+              (float)(ties[(size_t)b] + (max_out[b * ld_max + f] == 0.f ? 1 : 0));
+        if (max_first_row) max_first_row[b * feat + f] = first[(size_t)b];
+      }
+    }
+  }
+}
+
+// dx[i] = dmean[b] / count_b + (x[i] == max[b] ? dmax[b] / max_divisor[b] : 0);
+// with max_first_row the max term goes to that row alone (x.max(dim)).
+void sldm_cpu_segment_pool_bwd(const float* x, int64_t ldx, const int64_t* batch, int64_t nrows,
+                               int64_t num_segments, int64_t feat, const float* dmean,
+                               int64_t ld_dmean, const float* max_out, int64_t ld_max,
+                               const float* dmax, int64_t ld_dmax, const float* max_divisor,
+                               const int32_t* max_first_row, float* dx, int64_t ld_dx) {
+  std::vector<int64_t> count((size_t)num_segments, 0);
+  for (int64_t i = 0; i < nrows; ++i) ++count[(size_t)batch[i]];
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < nrows; ++i) {
+    const int64_t b = batch[i];
+    const float cnt = (float)(count[(size_t)b] > 0 ? count[(size_t)b] : 1);
+    for (int64_t f = 0; f < feat; ++f) {
+      float g = dmean ? dmean[b * ld_dmean + f] / cnt : 0.f;
+      if (dmax) {
+        if (max_first_row) {
+          if (max_first_row[b * feat + f] == (int32_t)i) g += dmax[b * ld_dmax + f];
+        } else if (x[i * ldx + f] == max_out[b * ld_max + f]) {
+          g += dmax[b * ld_dmax + f] / max_divisor[b * feat + f];
+        }
+      }
+      dx[i * ld_dx + f] = g;
+    }
+  }
+}
+
+int sldm_cpu_abi_version(void) { return 2; }
 
 }  // extern "C"

@@ -33,6 +33,10 @@ _SIG = {
                                  ctypes.c_uint64, _i64, _vp, _vp, _vp]),
     "sldm_cpu_post_bwd": (None, [_vp, _vp, _vp, _i64, _i64, _vp, _vp, _f, _f, ctypes.c_uint64,
                                  _i64, _vp, _vp, _vp, _vp]),
+    "sldm_cpu_segment_pool": (None, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp,
+                                     _vp]),
+    "sldm_cpu_segment_pool_bwd": (None, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64,
+                                         _vp, _i64, _vp, _vp, _vp, _i64]),
 }
 _lock = threading.Lock()
 _lib = None
@@ -101,51 +105,106 @@ def gather_rows(x, rowptr, col, num_rows, mean, addend=None):
     return out
 
 
-class _CpuLayerFn(torch.autograd.Function):
-    """One SageBlock layer on the host kernels (sageblock.py:18-19)."""
+def as_f32(x: torch.Tensor) -> torch.Tensor:
+    if x.dtype != torch.float32:
+        raise TypeError(f"SageBlock on CPU computes in float32 (the reference's dtype), "
+                        f"got {x.dtype}")
+    return x.contiguous()
+
+
+def scale_rows_by_inv_deg_(g: torch.Tensor, rowptr: torch.Tensor) -> torch.Tensor:
+    load().sldm_cpu_scale_rows_by_inv_deg(g.data_ptr(), g.size(1), rowptr.data_ptr(), g.size(0),
+                                          g.size(1))
+    return g
+
+
+def layer_fwd(x, rowptr, col, wl, bl, wr, gamma, beta, slope, drop_p, seed, eps):
+    """One SageBlock layer on the host kernels (sageblock.py:18-19): the CPU
+    implementation of ``torch.ops.sldm.sage_layer`` -> (out, agg, xhat, rstd)."""
+    n = x.size(0)
+    agg = gather_rows(x, rowptr, col, n, True)
+    h = torch.mm(agg, wl.detach().t())
+    h.addmm_(x, wr.detach().t())
+    fo = h.size(1)
+    out = torch.empty(n, fo)
+    xhat = torch.empty(n, fo)
+    rstd = torch.empty(n)
+    # bound to locals: a converted copy must outlive the C call
+    bias_, gamma_, beta_ = _f32(bl), _f32(gamma), _f32(beta)
+    load().sldm_cpu_post_fwd(h.data_ptr(), fo, n, fo, _p(bias_), gamma_.data_ptr(),
+                             beta_.data_ptr(), float(eps), float(slope), float(drop_p),
+                             seed & (2**64 - 1), 0, out.data_ptr(), xhat.data_ptr(),
+                             rstd.data_ptr())
+    return out, agg, xhat, rstd
+
+
+def layer_bwd(dout, x, agg, xhat, rstd, rowptr, t_rowptr, t_col, wl, wr, gamma, beta, slope,
+              drop_p, seed, need_dx):
+    """CPU implementation of ``torch.ops.sldm.sage_layer_bwd`` ->
+    (dx, dW_l, db_l, dW_r, dgamma, dbeta); dx has 0 elements unless need_dx."""
+    n, fo = xhat.shape
+    dout = dout.float().contiguous()
+    dh = torch.empty(n, fo)
+    dg, db, dbias = torch.empty(fo), torch.empty(fo), torch.empty(fo)
+    gamma_, beta_ = _f32(gamma), _f32(beta)
+    load().sldm_cpu_post_bwd(dout.data_ptr(), xhat.data_ptr(), rstd.data_ptr(), n, fo,
+                             gamma_.data_ptr(), beta_.data_ptr(), float(slope),
+                             float(drop_p), seed & (2**64 - 1), 0, dh.data_ptr(),
+                             dg.data_ptr(), db.data_ptr(), dbias.data_ptr())
+    dwl = torch.mm(dh.t(), agg)
+    dwr = torch.mm(dh.t(), x)
+    dx = x.new_empty(0)
+    if need_dx:
+        g = torch.mm(dh, wl.detach())
+        scale_rows_by_inv_deg_(g, rowptr)
+        dx_r = torch.mm(dh, wr.detach())
+        dx = gather_rows(g, t_rowptr, t_col, n, False, addend=dx_r)
+    return (dx, dwl.to(wl.dtype), dbias.to(wl.dtype), dwr.to(wr.dtype), dg.to(gamma.dtype),
+            db.to(beta.dtype))
+
+
+class PoolFn(torch.autograd.Function):
+    """global mean / max / mean||max pooling of CPU tensors (pool.py's CPU
+    mode): mode bit 1 mean, bit 2 max; ``first_arg``: batch=None routing of
+    the max gradient (to the first maximal row)."""
 
     @staticmethod
-    def forward(ctx, x, wl, bl, wr, gamma, beta, graph, slope, drop_p, seed, eps):
-        n = x.size(0)
-        agg = gather_rows(x, graph.rowptr, graph.col, n, True)
-        h = torch.mm(agg, wl.detach().t())
-        h.addmm_(x, wr.detach().t())
-        fo = h.size(1)
-        out = torch.empty(n, fo)
-        xhat = torch.empty(n, fo)
-        rstd = torch.empty(n)
-        # bound to locals: a converted copy must outlive the C call
-        bias_, gamma_, beta_ = _f32(bl), _f32(gamma), _f32(beta)
-        load().sldm_cpu_post_fwd(h.data_ptr(), fo, n, fo, _p(bias_), gamma_.data_ptr(),
-                                 beta_.data_ptr(), float(eps), float(slope), float(drop_p),
-                                 seed & (2**64 - 1), 0, out.data_ptr(), xhat.data_ptr(),
-                                 rstd.data_ptr())
-        ctx.save_for_backward(x, agg, xhat, rstd, wl, wr, gamma, beta)
-        ctx.graph, ctx.cfg = graph, (slope, drop_p, seed)
+    def forward(ctx, x, batch, num_segments: int, mode: int, first_arg: bool):
+        x = as_f32(x)
+        batch = batch.to(torch.int64).contiguous()
+        if batch.numel() and (int(batch.min()) < 0 or int(batch.max()) >= num_segments):
+            raise IndexError(f"batch holds a graph id outside [0, {num_segments})")
+        n, F = x.shape
+        B = int(num_segments)
+        mean, mx = bool(mode & 1), bool(mode & 2)
+        out = torch.empty(B, F * (2 if mean and mx else 1))
+        meanv = out[:, :F] if mean else None
+        maxv = out[:, F * (1 if mean else 0):] if mx else None
+        div = torch.empty(B, F) if mx and not first_arg else None
+        arg = torch.empty(B, F, dtype=torch.int32) if mx and first_arg else None
+        load().sldm_cpu_segment_pool(x.data_ptr(), x.stride(0), batch.data_ptr(), n, B, F,
+                                     _p(meanv), meanv.stride(0) if mean else 0, _p(maxv),
+                                     maxv.stride(0) if mx else 0, _p(div), _p(arg))
+        ctx.save_for_backward(x, batch, out)
+        ctx.aux, ctx.cfg = (div, arg), (B, mode)
         return out
 
     @staticmethod
-    def backward(ctx, dout):
-        x, agg, xhat, rstd, wl, wr, gamma, beta = ctx.saved_tensors
-        graph = ctx.graph
-        slope, drop_p, seed = ctx.cfg
-        n, fo = xhat.shape
-        dout = dout.float().contiguous()
-        dh = torch.empty(n, fo)
-        dg, db, dbias = torch.empty(fo), torch.empty(fo), torch.empty(fo)
-        gamma_, beta_ = _f32(gamma), _f32(beta)
-        load().sldm_cpu_post_bwd(dout.data_ptr(), xhat.data_ptr(), rstd.data_ptr(), n, fo,
-                                 gamma_.data_ptr(), beta_.data_ptr(), float(slope),
-                                 float(drop_p), seed & (2**64 - 1), 0, dh.data_ptr(),
-                                 dg.data_ptr(), db.data_ptr(), dbias.data_ptr())
-        dwl = torch.mm(dh.t(), agg)
-        dwr = torch.mm(dh.t(), x)
-        dx = None
-        if ctx.needs_input_grad[0]:
-            g = torch.mm(dh, wl.detach())
-            load().sldm_cpu_scale_rows_by_inv_deg(g.data_ptr(), g.size(1), graph.rowptr.data_ptr(),
-                                                  n, g.size(1))
-            dx_r = torch.mm(dh, wr.detach())
-            dx = gather_rows(g, graph.t_rowptr, graph.t_col, n, False, addend=dx_r)
-        return (dx, dwl.to(wl.dtype), dbias.to(wl.dtype), dwr.to(wr.dtype),
-                dg.to(gamma.dtype), db.to(beta.dtype), None, None, None, None, None)
+    def backward(ctx, gout):
+        if not ctx.needs_input_grad[0]:
+            return None, None, None, None, None
+        x, batch, out = ctx.saved_tensors
+        div, arg = ctx.aux
+        B, mode = ctx.cfg
+        n, F = x.shape
+        mean, mx = bool(mode & 1), bool(mode & 2)
+        g = gout.float().contiguous()
+        dmean = g[:, :F] if mean else None
+        dmax = g[:, F * (1 if mean else 0):] if mx else None
+        maxv = out[:, F * (1 if mean else 0):] if mx else None
+        dx = torch.empty_like(x)
+        load().sldm_cpu_segment_pool_bwd(
+            x.data_ptr(), x.stride(0), batch.data_ptr(), n, B, F, _p(dmean),
+            dmean.stride(0) if mean else 0, _p(maxv), maxv.stride(0) if mx else 0, _p(dmax),
+            dmax.stride(0) if mx else 0, _p(div), _p(arg), dx.data_ptr(), dx.stride(0))
+        return dx, None, None, None, None

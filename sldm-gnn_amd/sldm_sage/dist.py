@@ -116,8 +116,7 @@ class HipBackend:
     def post_bwd(dout, xhat, rstd, gamma, beta, slope, drop_p, seed, zout, row_offset):
         from . import ops
         return ops.post_bwd(dout, xhat, rstd, gamma, beta, slope, drop_p, seed,
-                            dh_dtype=xhat.dtype, zout=ops.branch_source(zout),
-                            row_offset=row_offset)
+                            dh_dtype=xhat.dtype, row_offset=row_offset)
 
     @staticmethod
     def bwd_data(dh, wl, wr, rowptr):

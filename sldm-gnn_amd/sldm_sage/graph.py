@@ -48,14 +48,36 @@ class SageGraph:
     col: torch.Tensor               # [E]   sources, original edge order per row
     t_rowptr: torch.Tensor | None   # [N+1] by source (backward)
     t_col: torch.Tensor | None      # [E]   destinations
-    order: torch.Tensor | None = None     # longest-first schedule of rowptr rows (SLDM_SKEW=order)
-    t_order: torch.Tensor | None = None   # same for t_rowptr
     hub: HubPlan | None = None            # high-degree split of rowptr rows (skewed graphs)
     t_hub: HubPlan | None = None          # same for t_rowptr
+    _packed: tuple | None = None
 
     @property
     def device(self) -> torch.device:
         return self.rowptr.device
+
+    def packed(self) -> tuple[list, list]:
+        """The graph as the ``(Tensor[12], int[9])`` pair the ``torch.ops.sldm``
+        operators take: [rowptr, col, t_rowptr, t_col, then the hub plan of
+        the rows and of the transpose rows (hub_rows, chunk_ptr, chunk_row,
+        chunk_beg each)] -- absent entries have 0 elements -- and
+        [has_transpose, num_hubs, num_chunks, chunk_len, max_deg, and the
+        same four for the transpose].  Built once per graph."""
+        if self._packed is None:
+            none = self.rowptr.new_empty(0)
+            ts = [self.rowptr, self.col,
+                  self.t_rowptr if self.t_rowptr is not None else none,
+                  self.t_col if self.t_col is not None else none]
+            meta = [int(self.t_rowptr is not None)]
+            for h in (self.hub, self.t_hub):
+                if h is None:
+                    ts += [none] * 4
+                    meta += [0, 0, 1, 0]
+                else:
+                    ts += [h.hub_rows, h.chunk_ptr, h.chunk_row, h.chunk_beg]
+                    meta += [h.num_hubs, h.num_chunks, h.chunk_len, h.max_deg]
+            self._packed = (ts, meta)
+        return self._packed
 
     def in_degree(self) -> torch.Tensor:
         return self.rowptr[1:] - self.rowptr[:-1]
@@ -64,14 +86,12 @@ class SageGraph:
 # Skew handling (power-law graphs).  Graphs below HUB_MIN_EDGES are
 # launch-bound (per-batch vehicle graphs: ~10^4 edges) and skip it -- and its
 # host sync -- entirely.  SLDM_SKEW: "split" (default: hub rows split into
-# chunks), "order" (round 1's longest-first schedule) or "none".
+# chunks) or "none".
 HUB_MIN_EDGES = int(os.environ.get("SLDM_HUB_MIN_EDGES", str(1 << 20)))
 HUB_CHUNK = 256          # edges per hub chunk (one row group sums one chunk)
 
 
 def _skew_mode() -> str:
-    if os.environ.get("SLDM_NO_SCHEDULE") == "1":
-        return "none"
     return os.environ.get("SLDM_SKEW", "split")
 
 
@@ -116,16 +136,10 @@ def build_graph(edge_index: torch.Tensor, num_nodes: int, transpose: bool = True
             "(the reference's index_select/scatter would raise as well)")
     if skew_check:
         thr = hub_threshold(num_nodes, E)
-        if mode == "order":
-            if vals[1] > max(64, 8 * E / num_nodes):
-                g.order = ops.degree_order(rowptr)
-            if t_rowptr is not None and vals[2] > max(64, 8 * E / num_nodes):
-                g.t_order = ops.degree_order(t_rowptr)
-        else:
-            if vals[1] > thr:
-                g.hub = hub_plan(rowptr, thr)
-            if t_rowptr is not None and vals[2] > thr:
-                g.t_hub = hub_plan(t_rowptr, thr)
+        if vals[1] > thr:
+            g.hub = hub_plan(rowptr, thr)
+        if t_rowptr is not None and vals[2] > thr:
+            g.t_hub = hub_plan(t_rowptr, thr)
     return g
 
 

@@ -22,10 +22,28 @@ _timing_names = None
 
 def set_timing_hook(hook, names=None) -> None:
     """Bracket launches with HIP events and hand them to ``hook`` (bench.py);
-    ``names``: only these ops (None: all).  Diagnostic plumbing."""
+    ``names``: only these ops (None: all).  Diagnostic plumbing.  Launches
+    made from Python here call ``hook(name, start_event, end_event, units)``;
+    those made inside the ``torch.ops.sldm`` operators are recorded in C++ and
+    reach ``hook.add_ms(name, ms, units)`` on :func:`flush_timing` (also
+    called when the hook is removed)."""
     global _timing_hook, _timing_names
+    from . import torch_ops
+    if hook is None and _timing_hook is not None:
+        flush_timing()
     _timing_hook = hook
     _timing_names = None if names is None else frozenset(names)
+    torch_ops.timing_set(hook is not None, names)
+
+
+def flush_timing() -> None:
+    """Hand the launches recorded inside the C++ operators to the hook (waits
+    for their end events)."""
+    from . import torch_ops
+    recs = torch_ops.timing_take()
+    if _timing_hook is not None:
+        for name, ms, units in recs:
+            _timing_hook.add_ms(name, ms, units)
 
 
 def dtype_code(t: torch.Tensor) -> int:
@@ -426,21 +444,6 @@ def cols_unpack(blocks: torch.Tensor, num_rows: int, num_blocks: int, block_cols
             addend.stride(0) if addend is not None else 0, out.data_ptr(), out.stride(0),
             _stream(dev)), "sldm_cols_unpack")
     return out
-
-
-def branch_source(out: torch.Tensor) -> torch.Tensor | None:
-    """What the post backward reads to pick the activation branch.
-
-    Default None: sign(y) is recomputed from the saved xhat as
-    y = fma(xhat, gamma, beta) -- bit-identical to the forward's y for fp32
-    storage; with bf16 storage only |y| within half an xhat ulp of 0 can flip
-    (the elements whose sign bf16 already leaves undetermined against an fp32
-    reference).  SLDM_ACT_BRANCH_FROM_OUTPUT=1 reads the saved layer output
-    instead (exact sign in bf16 too, one more [N, F] read per layer)."""
-    return out if _BRANCH_FROM_OUTPUT else None
-
-
-_BRANCH_FROM_OUTPUT = __import__("os").environ.get("SLDM_ACT_BRANCH_FROM_OUTPUT") == "1"
 
 
 def post_bwd(dout: torch.Tensor, xhat: torch.Tensor, rstd: torch.Tensor, gamma, beta,

@@ -112,71 +112,45 @@ def _zeros_batch(n: int, dev: torch.device) -> torch.Tensor:
     return t
 
 
-def _pool_fwd(x: torch.Tensor, seg: _Segments, mode: int, first_arg: bool):
-    dev = ops._require_gpu(x, seg.rowptr)
-    B, F = seg.num_segments, x.size(1)
-    dt = ops.dtype_code(x)
-    lib = _lib.load()
-    out = torch.empty(B, F * (2 if mode == _MEAN | _MAX else 1), dtype=x.dtype, device=dev)
-    mean = out[:, :F] if mode & _MEAN else None
-    mx = out[:, F * (1 if mode & _MEAN else 0):] if mode & _MAX else None
-    div = (torch.empty(B, F, dtype=torch.float32, device=dev)
-           if mode & _MAX and not first_arg else None)
-    arg = torch.empty(B, F, dtype=torch.int32, device=dev) if mode & _MAX and first_arg else None
-    ws_bytes = lib.sldm_segment_pool_workspace_bytes(seg.num_pieces, F)
-    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-    with ops._Timed("pool_fwd", x.numel() * x.element_size()):
-        _lib.check(lib.sldm_segment_pool(
-            dt, x.data_ptr(), x.stride(0), seg.rowptr.data_ptr(), seg.member.data_ptr(), B,
-            seg.piece_ptr.data_ptr(), seg.num_pieces, F, ops._ptr(mean),
-            mean.stride(0) if mean is not None else 0, ops._ptr(mx),
-            mx.stride(0) if mx is not None else 0, ops._ptr(div), ops._ptr(arg), ws.data_ptr(),
-            ws_bytes, ops._stream(dev)), "sldm_segment_pool")
-    return out, mx, div, arg
-
-
 class _PoolFn(torch.autograd.Function):
+    """``torch.ops.sldm.segment_pool`` / ``segment_pool_bwd`` (pool.hip)."""
+
     @staticmethod
     def forward(ctx, x, seg: _Segments, mode: int, first_arg: bool):
+        from . import torch_ops
         x = x.contiguous()
-        out, mx, div, arg = _pool_fwd(x, seg, mode, first_arg)
+        out, div, arg = torch_ops.load().segment_pool(x, seg.rowptr, seg.member, seg.piece_ptr,
+                                                      seg.num_segments, seg.num_pieces, mode,
+                                                      first_arg)
         ctx.seg, ctx.mode = seg, mode
-        if mode & _MAX:
-            ctx.save_for_backward(x, mx, div, arg)
-        else:
-            ctx.save_for_backward(x)
+        ctx.save_for_backward(x, out, div, arg)
         return out
 
     @staticmethod
     def backward(ctx, gout):
         if not ctx.needs_input_grad[0]:
             return None, None, None, None
-        seg, mode = ctx.seg, ctx.mode
-        x = ctx.saved_tensors[0]
-        mx, div, arg = ctx.saved_tensors[1:] if mode & _MAX else (None, None, None)
-        F = x.size(1)
-        g = gout.to(x.dtype)
-        if g.stride(-1) != 1:
-            g = g.contiguous()
-        dmean = g[:, :F] if mode & _MEAN else None
-        dmax = g[:, F * (1 if mode & _MEAN else 0):] if mode & _MAX else None
-        dev = x.device
-        dx = torch.empty_like(x)
-        n = x.size(0)
-        with ops._Timed("pool_bwd", 2 * x.numel() * x.element_size()):
-            _lib.check(_lib.load().sldm_segment_pool_bwd(
-                ops.dtype_code(x), x.data_ptr(), x.stride(0), seg.seg_of.data_ptr(),
-                seg.rowptr.data_ptr(), n, F, ops._ptr(dmean),
-                dmean.stride(0) if dmean is not None else 0, ops._ptr(mx),
-                mx.stride(0) if mx is not None else 0, ops._ptr(dmax),
-                dmax.stride(0) if dmax is not None else 0, ops._ptr(div), ops._ptr(arg),
-                dx.data_ptr(), dx.stride(0), ops._stream(dev)), "sldm_segment_pool_bwd")
+        x, out, div, arg = ctx.saved_tensors
+        seg = ctx.seg
+        dx = torch.ops.sldm.segment_pool_bwd(gout, x, out, div, arg, seg.seg_of, seg.rowptr,
+                                             ctx.mode)
         return dx, None, None, None
 
 
 def _pool(x: torch.Tensor, batch, size, mode: int) -> torch.Tensor:
     if x.dim() != 2:
         raise ValueError(f"pooling expects x [N, F], got {tuple(x.shape)}")
+    if x.device.type == "cpu":
+        # the reference's CPU mode (main.py:58): the host library
+        from . import cpu
+        first = batch is None
+        if first:
+            batch, size = torch.zeros(x.size(0), dtype=torch.int64), (1 if size is None else size)
+        if size is None:
+            size = int(batch.max().item()) + 1 if batch.numel() else 0
+        if x.size(0) == 0 or x.size(1) == 0:
+            return x.new_zeros(int(size), x.size(1) * (2 if mode == _MEAN | _MAX else 1))
+        return cpu.PoolFn.apply(x, batch, int(size), mode, first)
     ops._require_gpu(x, batch)
     seg = _segments(x, batch, size)
     if x.size(0) == 0 or x.size(1) == 0:

@@ -14,7 +14,8 @@ level — constructor ``SageBlock(hdims, dropout=None, negative_slope=None)``,
 work unchanged.
 
 Each layer (PyG 2.7.0 SAGEConv(mean) + LayerNorm + act + Dropout) runs as
-one autograd node over the C ABI:
+one PyTorch custom operator (torch.ops.sldm.sage_layer; in training the whole
+stack as sage_stack_fwd / sage_stack_bwd) over the C ABI:
   forward : gather-mean over CSR-by-dst -> [agg|x]·[W_l|W_r]^T -> bias+LN+act+dropout
   backward: LN/act/dropout bwd -> dh·[W_l|W_r] -> dW -> 1/deg prescale ->
             transpose gather + lin_r grad
@@ -26,7 +27,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from . import dense, ops
+from . import ops, torch_ops
 from .graph import SageGraph, get_graph
 
 
@@ -71,168 +72,61 @@ def _new_seed(device: torch.device | None = None) -> int:
     return _splitmix64(gen.initial_seed() ^ _splitmix64(off)) & (2**62 - 1)
 
 
-class _SageLayerFn(torch.autograd.Function):
-    """One SageBlock layer: SAGEConv(mean) -> LayerNorm -> act -> dropout."""
-
-    @staticmethod
-    def forward(ctx, x, wl, bl, wr, gamma, beta, graph: SageGraph, slope: float, drop_p: float,
-                seed: int, eps: float):
-        n = x.size(0)
-        agg = ops.gather_rows(x, graph.rowptr, graph.col, n, mean=True, name="gather_fwd",
-                              order=graph.order, hub=graph.hub)
-        needs_grad = any(ctx.needs_input_grad[:6])
-        wcat = dense.weight_cat(wl, wr, x.dtype)
-        out, xhat, rstd = dense.sage_layer_fwd(agg, x, wl, bl, wr, gamma, beta, eps, slope,
-                                               drop_p, seed, save=needs_grad, wcat=wcat)
-        if needs_grad:
-            ctx.wcat = wcat
-            # `out` is saved too (it is the next layer's input anyway): with
-            # SLDM_ACT_BRANCH_FROM_OUTPUT=1 its sign picks the activation
-            # branch in the backward (ops.branch_source).
-            ctx.save_for_backward(x, agg, xhat, rstd, wl, wr, gamma, beta, out)
-            ctx.graph = graph
-            ctx.cfg = (slope, drop_p, seed)
-        return out
-
-    @staticmethod
-    def backward(ctx, dout):
-        x, agg, xhat, rstd, wl, wr, gamma, beta, out = ctx.saved_tensors
-        graph: SageGraph = ctx.graph
-        slope, drop_p, seed = ctx.cfg
-        dh, dgamma, dbeta, dbl = ops.post_bwd(dout, xhat, rstd, gamma, beta, slope, drop_p, seed,
-                                              dh_dtype=x.dtype, zout=ops.branch_source(out))
-        dwl, dwr = dense.sage_linear_bwd_weight(dh, agg, x)
-        dx = None
-        if ctx.needs_input_grad[0]:
-            if graph.t_rowptr is None:
-                raise RuntimeError("SageGraph was built without its transpose; rebuild with "
-                                   "transpose=True for backward")
-            # [dAgg/deg | dx_root] in one MFMA pass, then the transpose gather
-            # adds the root-path gradient as it sums over out-edges.
-            g, dx_r = dense.sage_linear_bwd_data(dh, wl, wr, graph.rowptr, wcat=ctx.wcat)
-            dx = ops.gather_rows(g, graph.t_rowptr, graph.t_col, x.size(0), mean=False,
-                                 order=graph.t_order, hub=graph.t_hub,
-                                 addend=dx_r, name="gather_bwd")
-        return (dx, dwl.to(wl.dtype), dbl.to(wl.dtype), dwr.to(wr.dtype),
-                dgamma.to(gamma.dtype), dbeta.to(beta.dtype), None, None, None, None, None)
-
-
 # Training runs the stack as one autograd node with fused layer boundaries
-# (_SageStackFn); False (or SLDM_FUSE_BOUNDARIES=0) selects one node per layer
-# (_SageLayerFn) -- same results, for A/B comparisons and the tests.
+# (_SageStackFn); False (or SLDM_FUSE_BOUNDARIES=0) runs one differentiable
+# operator per layer (torch.ops.sldm.sage_layer) -- same results, for A/B
+# comparisons and the tests.
 FUSE_BOUNDARIES = __import__("os").environ.get("SLDM_FUSE_BOUNDARIES", "1") != "0"
-# Opt-in (SLDM_OVERLAP_DW=1): weight gradients (dW = dh^T [agg | h]) on a side
-# stream, concurrent with the same layer's dX GEMM and transpose gather.  At C4
-# it measured 70.0-70.5 vs 70.5-71.2 ms/step in the same call, and one of two
-# runs took 168 ms/step (the caching allocator holding the cross-stream blocks
-# of 5-GB tensors) -- not worth the risk as the default.
-OVERLAP_DW = __import__("os").environ.get("SLDM_OVERLAP_DW", "0") == "1"
-_SIDE_STREAMS: dict = {}
 
 
-def _side_stream(dev: torch.device):
-    st = _SIDE_STREAMS.get(dev.index)
-    if st is None:
-        st = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(dev)
-    return st
+def sage_layer(x, graph: SageGraph, wl, bl, wr, gamma, beta, slope: float, drop_p: float,
+               seed: int, eps: float) -> torch.Tensor:
+    """One SageBlock layer, SAGEConv(mean) -> LayerNorm -> act -> dropout, as
+    the dispatcher operator ``torch.ops.sldm.sage_layer`` (differentiable:
+    its backward is registered with torch.library.register_autograd; ROCm and
+    CPU tensors take their own kernels)."""
+    sldm = torch_ops.load()
+    gl, gm = graph.packed()
+    save = torch.is_grad_enabled() and any(
+        t is not None and t.requires_grad for t in (x, wl, bl, wr, gamma, beta))
+    return sldm.sage_layer(x, gl, gm, wl, bl, wr, gamma, beta, slope, drop_p, seed, eps, save)[0]
 
 
 class _SageStackFn(torch.autograd.Function):
-    """All layers of a SageBlock as one autograd node, so the backward can fuse
-    each layer boundary: the transpose gather of layer l and the LayerNorm /
-    act / dropout backward of layer l-1 run as one kernel (gather_post.hip)
-    and the input gradient of layer l never reaches HBM.  Forward and every
-    per-layer operation are those of :class:`_SageLayerFn`; the results are
-    bit-identical to it (dh from the fused kernel equals post_bwd of the
-    gathered gradient; only the fp32 column sums of dgamma / dbeta / dbias are
-    summed in a different row order)."""
+    """All layers of a SageBlock as one autograd node over two operators,
+    ``torch.ops.sldm.sage_stack_fwd`` / ``sage_stack_bwd`` (one C++ call per
+    direction), so the backward can fuse each layer boundary: the transpose
+    gather of layer l and the LayerNorm / act / dropout backward of layer l-1
+    run as one kernel (gather_post.hip) and the input gradient of layer l
+    never reaches HBM.  Results are bit-identical to the per-layer operator
+    (dh from the fused kernel equals post_bwd of the gathered gradient; only
+    the fp32 column sums of dgamma / dbeta / dbias are summed in a different
+    row order)."""
 
     @staticmethod
     def forward(ctx, x, graph: SageGraph, cfgs, *params):
-        n = x.size(0)
-        saved, wcats = [], []
-        h = x
-        for i, (slope, drop_p, seed, eps) in enumerate(cfgs):
-            wl, bl, wr, gamma, beta = params[5 * i: 5 * i + 5]
-            agg = ops.gather_rows(h, graph.rowptr, graph.col, n, mean=True, name="gather_fwd",
-                                  order=graph.order, hub=graph.hub)
-            wcat = dense.weight_cat(wl, wr, h.dtype)
-            out, xhat, rstd = dense.sage_layer_fwd(agg, h, wl, bl, wr, gamma, beta, eps, slope,
-                                                   drop_p, seed, save=True, wcat=wcat)
-            saved += [h, agg, xhat, rstd]
-            wcats.append(wcat)
-            h = out
-        ctx.save_for_backward(*saved, *params)
-        ctx.wcats = wcats
-        ctx.graph, ctx.cfgs, ctx.nl = graph, cfgs, len(cfgs)
-        return h
+        sldm = torch_ops.load()
+        gl, gm = graph.packed()
+        slopes = [c[0] for c in cfgs]
+        drops = [c[1] for c in cfgs]
+        seeds = [c[2] for c in cfgs]
+        eps = [c[3] for c in cfgs]
+        res = sldm.sage_stack_fwd(x, gl, gm, params, slopes, drops, seeds, eps, True)
+        ctx.save_for_backward(*res[1:], *params)
+        ctx.graph, ctx.cfg, ctx.nl = graph, (slopes, drops, seeds), len(cfgs)
+        return res[0]
 
     @staticmethod
     def backward(ctx, dout):
-        nl, graph, cfgs = ctx.nl, ctx.graph, ctx.cfgs
+        nl = ctx.nl
         st = ctx.saved_tensors
-        acts, params = st[: 4 * nl], st[4 * nl:]
-        if graph.t_rowptr is None:
-            raise RuntimeError("SageGraph was built without its transpose; rebuild with "
-                               "transpose=True for backward")
-        grads = [None] * len(params)
-        x_in = acts[0]
-        top = nl - 1
-        slope, drop_p, seed, _ = cfgs[top]
-        wl, bl, wr, gamma, beta = params[5 * top: 5 * top + 5]
-        dh, dgamma, dbeta, dbl = ops.post_bwd(dout, acts[4 * top + 2], acts[4 * top + 3], gamma,
-                                              beta, slope, drop_p, seed, dh_dtype=x_in.dtype)
-        dx = None
-        main = torch.cuda.current_stream(dh.device)
-        side = _side_stream(dh.device) if OVERLAP_DW else None
-        side_out = []
-        for i in range(top, -1, -1):
-            h, agg = acts[4 * i], acts[4 * i + 1]
-            wl, bl, wr, gamma, beta = params[5 * i: 5 * i + 5]
-            if side is not None:
-                # inputs produced on the main stream; the caching allocator must
-                # not hand their blocks to main-stream allocations until the
-                # side stream is done with them (record_stream)
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    dwl, dwr = dense.sage_linear_bwd_weight(dh, agg, h)
-                    dwl, dwr = dwl.to(wl.dtype), dwr.to(wr.dtype)
-                for t in (dh, agg, h):
-                    t.record_stream(side)
-                side_out += [dwl, dwr]
-            else:
-                dwl, dwr = dense.sage_linear_bwd_weight(dh, agg, h)
-                dwl, dwr = dwl.to(wl.dtype), dwr.to(wr.dtype)
-            grads[5 * i: 5 * i + 5] = [dwl, dbl.to(wl.dtype), dwr, dgamma.to(gamma.dtype),
-                                       dbeta.to(beta.dtype)]
-            if i == 0 and not ctx.needs_input_grad[0]:
-                break
-            g, dx_r = dense.sage_linear_bwd_data(dh, wl, wr, graph.rowptr, wcat=ctx.wcats[i])
-            if i == 0:
-                dx = ops.gather_rows(g, graph.t_rowptr, graph.t_col, h.size(0), mean=False,
-                                     order=graph.t_order, hub=graph.t_hub, addend=dx_r, name="gather_bwd")
-                break
-            # boundary: layer i's input gradient straight into layer i-1's post backward
-            slope, drop_p, seed, _ = cfgs[i - 1]
-            gamma_b, beta_b = params[5 * (i - 1) + 3], params[5 * (i - 1) + 4]
-            if graph.t_hub is not None:
-                # out-degree hubs: the split transpose gather, then the post
-                # backward (the fused kernel sums each row in one row group)
-                dxi = ops.gather_rows(g, graph.t_rowptr, graph.t_col, h.size(0), mean=False,
-                                      hub=graph.t_hub, addend=dx_r, name="gather_bwd")
-                dh, dgamma, dbeta, dbl = ops.post_bwd(
-                    dxi, acts[4 * (i - 1) + 2], acts[4 * (i - 1) + 3], gamma_b, beta_b, slope,
-                    drop_p, seed, dh_dtype=x_in.dtype)
-                continue
-            dh, dgamma, dbeta, dbl = ops.gather_post_bwd(
-                g, graph.t_rowptr, graph.t_col, graph.t_order, dx_r, acts[4 * (i - 1) + 2],
-                acts[4 * (i - 1) + 3], gamma_b, beta_b, slope, drop_p, seed)
-        if side is not None:
-            # the weight grads are consumed on the main stream after this returns
-            main.wait_stream(side)
-            for t in side_out:
-                t.record_stream(main)
-        return (dx, None, None, *grads)
+        saved, params = st[: 4 * nl], st[4 * nl:]
+        slopes, drops, seeds = ctx.cfg
+        gl, gm = ctx.graph.packed()
+        need_dx = ctx.needs_input_grad[0]
+        grads = torch.ops.sldm.sage_stack_bwd(dout, saved, gl, gm, params, slopes, drops, seeds,
+                                              need_dx, True)
+        return (grads[0] if need_dx else None, None, None, *grads[1:])
 
 
 class SageConv(nn.Module):
@@ -254,8 +148,7 @@ class SageConv(nn.Module):
 
     def forward(self, x: torch.Tensor, edge_index) -> torch.Tensor:
         """Stand-alone conv (no post stack): lin_l(mean_j x_j) + lin_r(x)."""
-        graph = get_graph(edge_index, x.size(0), transpose=torch.is_grad_enabled())
-        agg = _MeanAggFn.apply(x, graph)
+        agg = sage_aggregate(x, edge_index)
         out = nn.functional.linear(agg.to(self.lin_l.weight.dtype), self.lin_l.weight,
                                    self.lin_l.bias)
         return out + nn.functional.linear(x.to(self.lin_r.weight.dtype), self.lin_r.weight)
@@ -264,29 +157,14 @@ class SageConv(nn.Module):
         return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, aggr=mean)"
 
 
-class _MeanAggFn(torch.autograd.Function):
-    """Mean neighbour aggregation alone (PyG propagate + MeanAggregation)."""
-
-    @staticmethod
-    def forward(ctx, x, graph: SageGraph):
-        ctx.graph = graph
-        ctx.n = x.size(0)
-        return ops.gather_rows(x, graph.rowptr, graph.col, x.size(0), mean=True, order=graph.order, hub=graph.hub,
-                               name="gather_fwd")
-
-    @staticmethod
-    def backward(ctx, g):
-        graph = ctx.graph
-        g = g.contiguous().clone()
-        ops.scale_rows_by_inv_deg_(g, graph.rowptr)
-        return ops.gather_rows(g, graph.t_rowptr, graph.t_col, ctx.n, mean=False, order=graph.t_order, hub=graph.t_hub,
-                               name="gather_bwd"), None
-
-
 def sage_aggregate(x: torch.Tensor, edge_index) -> torch.Tensor:
-    """Mean aggregation over in-edges (differentiable)."""
+    """Mean aggregation over in-edges (PyG propagate + MeanAggregation),
+    differentiable: ``torch.ops.sldm.mean_aggregate``."""
     graph = get_graph(edge_index, x.size(0), transpose=torch.is_grad_enabled())
-    return _MeanAggFn.apply(x, graph)
+    gl, gm = graph.packed()
+    if x.device.type == "cuda" and x.dtype not in (torch.float32, torch.bfloat16):
+        x = x.float()
+    return torch_ops.load().mean_aggregate(x, gl, gm)
 
 
 class SageBlock(nn.Module):
@@ -330,19 +208,19 @@ class SageBlock(nn.Module):
             layers.append(((conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, ln.weight,
                             ln.bias), (_act_slope(act), p, _new_seed(x.device) if p > 0 else 0,
                                        float(ln.eps))))
-        if grad and FUSE_BOUNDARIES and ops.branch_source(x) is None:
+        if grad and FUSE_BOUNDARIES:
             # training: one autograd node for the stack (fused layer boundaries)
             cfgs = tuple(c for _, c in layers)
             params = [t for w, _ in layers for t in w]
             return _SageStackFn.apply(x, graph, cfgs, *params)
         for (wl, bl, wr, gamma, beta), (slope, p, seed, eps) in layers:
-            x = _SageLayerFn.apply(x, wl, bl, wr, gamma, beta, graph, slope, p, seed, eps)
+            x = sage_layer(x, graph, wl, bl, wr, gamma, beta, slope, p, seed, eps)
         return x
 
     def _forward_cpu(self, x: torch.Tensor, edge_index) -> torch.Tensor:
-        """CPU tensors (the reference's DEVICE='cpu' mode): the host kernels of
-        cpu.py, fp32 (the reference's dtype), one autograd node per layer."""
-        from .cpu import _CpuLayerFn
+        """CPU tensors (the reference's DEVICE='cpu' mode): the same operator,
+        dispatched to the host kernels of cpu.py; fp32 (the reference's
+        dtype), one differentiable operator call per layer."""
         if x.dtype != torch.float32:
             raise TypeError(f"SageBlock on CPU computes in float32 (the reference's dtype), "
                             f"got {x.dtype}")
@@ -357,9 +235,8 @@ class SageBlock(nn.Module):
             ln, act, drop = post[0], post[1], post[2]
             p = _drop_p(drop)
             seed = _cpu_seed() if p > 0 else 0
-            x = _CpuLayerFn.apply(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight,
-                                  ln.weight, ln.bias, graph, _act_slope(act), p, seed,
-                                  float(ln.eps))
+            x = sage_layer(x, graph, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight,
+                           ln.weight, ln.bias, _act_slope(act), p, seed, float(ln.eps))
         return x
 
 

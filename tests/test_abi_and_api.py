@@ -101,7 +101,7 @@ def test_cpu_library_exports_header():
     hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
     declared = sorted(set(re.findall(r"\b(sldm_cpu_[a-z0-9_]+)\s*\(", hdr)))
     lib = cpu.load()
-    assert len(declared) == 6
+    assert len(declared) == 8
     for name in declared:
         assert hasattr(lib, name) and name in cpu.exported_symbols(), name
-    assert lib.sldm_cpu_abi_version() == 1
+    assert lib.sldm_cpu_abi_version() == 2

@@ -57,6 +57,38 @@ def test_oracle_matches_loop_formulation():
         torch.testing.assert_close(out[s, f:], rows.max(0)[0])
 
 
+# ------------------------------------------- host library (CPU tensors) --
+@pytest.mark.parametrize("mode", ["mean", "max", "double"])
+def test_cpu_pool_matches_oracle(mode):
+    """sldm_sage pooling on CPU tensors (the reference's DEVICE='cpu' mode,
+    libsldm_sage_cpu.so): forward bit-equal to the oracle's scatter order,
+    gradients equal (ties, maxima of 0, empty graphs, batch=None)."""
+    import sldm_sage
+    fn = sldm_sage.global_pool(mode)
+    ref = {"mean": R.global_mean_pool, "max": R.global_max_pool,
+           "double": R.global_mean_max_pool}[mode]
+    g = torch.Generator().manual_seed(3)
+    n, f, B = 300, 7, 9
+    x = torch.randn(n, f, generator=g)
+    x[::5] = x[::5].round()                     # ties
+    x[:, 2] = -x[:, 2].abs()
+    x[::3, 2] = 0.0                             # maxima of exactly 0
+    b = torch.randint(0, B - 1, (n,), generator=g)     # graph B-1 stays empty
+    for batch, size in ((b, B), (torch.sort(b).values, None), (None, None)):
+        xa = x.clone().requires_grad_(True)
+        xb = x.clone().requires_grad_(True)
+        out = fn(xa, batch, size) if batch is not None else fn(xa, None)
+        want = ref(xb, batch, size)
+        if batch is None:       # x.mean(0) sums pairwise on the CPU: another order
+            torch.testing.assert_close(out, want, atol=1e-6, rtol=1e-6)
+        else:
+            assert torch.equal(out, want)
+        go = torch.randn(want.shape, generator=torch.Generator().manual_seed(4))
+        out.backward(go)
+        want.backward(go)
+        torch.testing.assert_close(xa.grad, xb.grad, atol=1e-6, rtol=1e-6)
+
+
 # -------------------------------------------------------------- GPU parity --
 def _batch(sizes, seed=0, shuffle=False):
     b = torch.cat([torch.full((s,), i, dtype=torch.int64) for i, s in enumerate(sizes)])

@@ -85,17 +85,6 @@ def main():
                                                    save), a.reps)
             add(f"dense_fwd p={p_} save={save}", ms, (2 * n * f + n * f * (2 if save else 1)) * s,
                 fl)
-        for var, env, p_ in [("ws", {"SLDM_WS_FWD": "1"}, 0.25),
-                             ("ws_xchg", {"SLDM_WS_FWD": "2"}, 0.25),
-                             ("ws_xchg", {"SLDM_WS_FWD": "2"}, 0.0),
-                             ("ws_pipe", {"SLDM_WS_FWD": "3"}, 0.25),
-                             ("ws_pipe", {"SLDM_WS_FWD": "3"}, 0.0)]:
-            os.environ.update(env)
-            ms = timeit(lambda: ops.sage_dense_fwd(agg, x, wcat, b, gam, bet, 1e-5, 0.1, p_, 7,
-                                                   True), a.reps)
-            add(f"dense_fwd p={p_} save=True {var}", ms, 4 * n * f * s, fl)
-            for k in env:
-                os.environ.pop(k)
     if want("nt"):
         add("gemm_nt_rowscale N=2f", timeit(lambda: ops.gemm_nt_rowscale(dh, wt, gr.rowptr, f),
                                             a.reps), (n * f + n * 2 * f) * s, fl)
@@ -125,14 +114,6 @@ def main():
         add("torch cat 2R:2W [N,2F]", timeit(lambda: torch.cat([dh, x], 1, out=c2), a.reps),
             4 * n * f * s)
         del c, c2
-    if want("postring"):
-        out, xh, rs = ops.post_fwd(dh, None, gam, bet, 1e-5, 0.1, 0.0, 0, dt, True)
-        for ring in ("0", "1"):
-            os.environ["SLDM_POST_RING"] = ring
-            add(f"post_bwd p=0.25 ring={ring}",
-                timeit(lambda: ops.post_bwd(dh, xh, rs, gam, bet, 0.1, 0.25, 3, dt), a.reps),
-                3 * n * f * s)
-        os.environ.pop("SLDM_POST_RING")
     if want("post"):
         out, xh, rs = ops.post_fwd(dh, None, gam, bet, 1e-5, 0.1, 0.0, 0, dt, True)
         for p_, zo in [(0.0, None), (0.25, None), (0.25, out)]:
@@ -144,10 +125,10 @@ def main():
         # layer boundary), and the plain transpose gather with an addend
         xh_, rs_ = dh, torch.rand(n, device=dev) + 0.5
         add("gather_post_bwd", timeit(lambda: ops.gather_post_bwd(
-            agg, gr.t_rowptr, gr.t_col, gr.t_order, x, xh_, rs_, gam, bet, 0.1, 0.25, 5), a.reps),
+            agg, gr.t_rowptr, gr.t_col, None, x, xh_, rs_, gam, bet, 0.1, 0.25, 5), a.reps),
             e * (4 + f * s) + 4 * n * f * s)
         add("gather_bwd (sum + addend)", timeit(lambda: ops.gather_rows(
-            agg, gr.t_rowptr, gr.t_col, n, False, addend=x, order=gr.t_order), a.reps),
+            agg, gr.t_rowptr, gr.t_col, n, False, addend=x, order=None), a.reps),
             e * (4 + f * s) + 2 * n * f * s)
     if want("concurrent"):
         # forward gather and dense forward on two streams at once (independent
