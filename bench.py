@@ -56,7 +56,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HBM_COPY_GBS = 6290.0   # measured float4-copy ceiling (MI355X_MICROARCH.md)
 MFMA_PEAK_TFLOPS = {torch.bfloat16: 2500.0, torch.float32: 157.3}   # dense, same guide
 BREAKDOWN_STEPS = 2      # untimed steps with every op bracketed (the "kernels" table)
-PMC_SUMMARY = "r2d_c4_pmc_traffic.json"   # latest committed PMC passes (tools/profile_round.sh)
+PMC_SUMMARY = "r3_c4_pmc_traffic.json"   # latest committed PMC passes (tools/profile_round.sh)
 
 
 class KernelTimer:
