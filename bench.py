@@ -3,7 +3,7 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4] [--no-cpu-baseline]
 
 One "step" = SageBlock.forward(x, edge_index) + backward of a fixed upstream
-gradient over one synthetic graph (SURVEY.md §8d), dropout 0.25 in training
+gradient over one synthetic graph, dropout 0.25 in training
 mode, LeakyReLU(0.1) — the reference's training configuration (main.py:39-40).
 ``value`` = E·L / t_step (layer-edges per second, whole job).  Inputs are
 resident in HBM before the timed region; the CSR is built on the first
@@ -90,7 +90,7 @@ class KernelTimer:
 
 
 def make_graph(n, e, f, dtype, device, seed=0, kind="uniform", p_local=0.9, blocks=8):
-    """SURVEY.md §8d synthetic graph: src, dst uniform in [0, N) (duplicates and
+    """The synthetic benchmark graph: src, dst uniform in [0, N) (duplicates and
     self loops allowed).  kind="local" is the locality-structured variant: dst
     uniform, src drawn from dst's own block (N split into `blocks` contiguous
     ranges = the 8-GPU partition) with probability p_local, else uniform."""
@@ -98,7 +98,7 @@ def make_graph(n, e, f, dtype, device, seed=0, kind="uniform", p_local=0.9, bloc
     src = torch.randint(0, n, (e,), generator=g, device=device)
     dst = torch.randint(0, n, (e,), generator=g, device=device)
     if kind == "powerlaw":
-        # dst from a truncated power law over ranks, ids
+        # C5: dst from a truncated power law over ranks, ids
         # permuted by a seeded randperm so hubs are scattered; src uniform.
         u = torch.rand(e, generator=g, device=device, dtype=torch.float64)
         b = 1.0 - ZIPF_A
@@ -146,7 +146,7 @@ def available_cpus() -> dict:
 def cpu_baseline(cfg, threads, frac=10, budget_s=30.0):
     """The oracle (plain-torch restatement of PyG SAGEConv + SageBlock, fp32:
     the reference's ATen op sequence) on a bounded sample of the workload --
-    the same F and L, nodes and edges / ``frac`` (SURVEY §8d: E/10 when the
+    the same F and L, nodes and edges / ``frac`` (E/10 when the
     full graph's [E, F] message tensors do not fit) -- on ``threads`` host
     threads, one warm-up step, then timed steps until ``budget_s``."""
     from oracle.sage_ref import RefSageBlock, random_graph, set_synthetic_params
@@ -242,7 +242,7 @@ def torch_ops_gpu_baseline(blk, ei, x, gout, warmup=1, steps=2):
 
 
 # ---------------------------------------------------------------------------
-# Real-workload lines (VERDICT r1 "what's missing" 5; SURVEY §7 hard part (iv))
+# Real-workload lines
 # ---------------------------------------------------------------------------
 PACKS_PER_BATCH = 32          # main.py:22-26 batch_size
 VEHICLES = (200, 300)         # vehicles per pack (rcv.py:14 caps packs at ~300)
@@ -385,7 +385,7 @@ def bench_map(args, dev):
 def bench_gru(args, dev):
     """The model's GRU (grusage.py:66-71,160-161): nn.GRU(6 -> 96, 1 layer,
     batch_first) over [N, T=100, 6], N = 32 packs x 300 vehicles, fp32,
-    forward + backward of the last hidden state (MIOpen; SURVEY §8f row 4:
+    forward + backward of the last hidden state (MIOpen;
     measure before any hand kernel).  Roofline: the gate GEMMs' FLOP against
     the dense fp32 MFMA peak."""
     from sldm_sage import GRU
@@ -441,7 +441,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20,
-                    help="timed steps (SURVEY.md §8d: >= 20 after 3 warm-ups, median reported "
+                    help="timed steps (>= 20 after 3 warm-ups, median reported "
                          "as ms_per_step_median_rank0)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS) + sorted(SMALL_WORKLOADS),
@@ -668,7 +668,7 @@ def main():
     elapsed, kern_timed, dist_info, incl, step_ms, kern = run(args.graph, True)
     variant = None
     if world > 1 and args.graph == "uniform":
-        # also the locality-structured variant (block-community
+        # C4: also the locality-structured variant (block-community
         # graph, cut fraction stated) -- the regime where the exchange overlaps.
         torch.cuda.empty_cache()
         v_el, _, v_info, _, _, _ = run("local", False)
@@ -698,7 +698,7 @@ def main():
                     kernel="gather_rows_kernel (forward mean aggregation)",
                     avg_ms=round(g["avg_ms"], 4), launches=g["launches"],
                     bytes_per_launch=int(g["avg_bytes"]))
-    # SURVEY.md §8d full-step roofline: T* = (algorithmic bytes of every timed
+    # Full-step roofline: T* = (algorithmic bytes of every timed
     # kernel in a step) / HBM peak + (GEMM FLOP of a step) / dense MFMA peak,
     # reported as T*/t (N = 1; at N > 1 the per-rank work is not the whole graph).
     step_bytes = sum(v["avg_bytes"] * v["launches"] for v in kern.values()) / BREAKDOWN_STEPS
@@ -711,7 +711,7 @@ def main():
                          t_star_ms=round(t_star * 1e3, 3),
                          frac=round(t_star / (elapsed / args.steps), 4),
                          frac_vs_measured_copy=round(t_star_copy / (elapsed / args.steps), 4),
-                         note="T* = bytes/8 TB/s + FLOP/dense MFMA peak (SURVEY 8d); "
+                         note="T* = bytes/8 TB/s + FLOP/dense MFMA peak; "
                               "frac_vs_measured_copy prices bytes at the 6.29 TB/s copy ceiling")
     kernels = {k: dict(avg_ms=round(v["avg_ms"], 4), launches=v["launches"],
                        gbs=round(v["avg_bytes"] / (v["avg_ms"] * 1e-3) / 1e9, 1))

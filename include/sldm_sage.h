@@ -2,7 +2,7 @@
  * sldm_sage.h — C ABI of the MI355X-native SageBlock hot path (libsldm_sage.so).
  *
  * The reference path is pure Python over PyTorch + torch_geometric 2.7.0 and has
- * no FFI of its own (no native code in the reference).  Each entry
+ * no FFI of its own (there is no native code in the reference).  Each entry
  * point below replaces one step of what the reference executes per
  * SageBlock.forward (/root/reference/src/models/blocks/sageblock.py:16-20) and
  * its autograd backward; the replaced step is cited on each declaration.
@@ -41,7 +41,7 @@ int sldm_abi_version(void);
 const char* sldm_last_error(void);
 
 /* ---------------------------------------------------------------- graph ---
- * CSR build (SURVEY.md §8a A9/A10).  Replaces the per-call addressing of PyG
+ * CSR build.  Replaces the per-call addressing of PyG
  * 2.7.0 MessagePassing.propagate (x.index_select(0, edge_index[0]) and the
  * scatter at edge_index[1]; called from sageblock.py:18) with, built once:
  *   rowptr[N+1], col[E]      CSR by destination: sources of node i's in-edges
@@ -73,7 +73,7 @@ int sldm_degree_order(const int32_t* rowptr, int64_t num_nodes, int32_t* order,
  * Sums are fp32, accumulated in CSR order (bit-identical to PyG's CPU
  * scatter_add_ for fp32 input).
  * Forward (mean=1, CSR by dst) replaces PyG 2.7.0 x.index_select(0, src) +
- * MeanAggregation / utils.scatter(reduce='mean') (SURVEY.md §8a A4-A5).
+ * MeanAggregation / utils.scatter(reduce='mean').
  * Backward (mean=0, transpose CSR, x = inv_deg-prescaled dAgg, addend = the
  * lin_r input gradient) replaces autograd's gather + index_add_ (A8).
  * addend may be NULL; it has out's dtype.  row_order (nullable) is a row
@@ -85,7 +85,7 @@ int sldm_gather_rows(int x_dtype, const void* x, int64_t ldx,
                      int out_dtype, void* out, int64_t ldo, void* stream);
 
 /* sldm_gather_rows with high-degree rows split (BASELINE C5: power-law
- * in-degrees up to ~10^4; SURVEY.md §7 step 9).  Rows with degree > max_deg
+ * in-degrees up to ~10^4).  Rows with degree > max_deg
  * ("hubs", listed in hub_rows) are summed as fixed-length edge chunks:
  * chunk c covers CSR positions [chunk_beg[c], min(chunk_beg[c] + chunk_len,
  * rowptr[chunk_row[c]+1])) and is summed by its own row group into the fp32
@@ -247,7 +247,7 @@ int sldm_cols_unpack(int dtype, const void* blocks_src, int64_t num_rows, int64_
                      int64_t ld_rows, void* stream);
 
 /* ------------------------------------------------- graph-level readout ---
- * Global mean / max pooling over the batch vector (SURVEY.md §8f row 1):
+ * Global mean / max pooling over the batch vector:
  * replaces PyG 2.7.0 global_mean_pool / global_max_pool (grusage.py:3,
  * :119-127, :185), i.e. utils.scatter(x, batch, reduce='mean' | 'max') --
  * zeros(B,F).scatter_reduce_(0, batch, x, 'amax', include_self=False) on the
@@ -283,7 +283,7 @@ int sldm_segment_pool_bwd(int dtype, const void* x, int64_t ldx, const int64_t* 
                           int64_t ld_dx, void* stream);
 
 /* ------------------------------------------------ graph construction ---
- * Radius edges of a vehicle pack (SURVEY.md §8f row 3), replacing the
+ * Radius edges of a vehicle pack, replacing the
  * O(V^2 T) pair loop of gbuilder.py:85-111 / :241-268: for i, for j != i,
  * d = per-frame XY distance over the frames both vehicles are present in
  * (presence > 0.5); if any and min(d) <= radius: edge (i, j) with attr
@@ -304,7 +304,7 @@ int sldm_radius_edges(const float* pos, int64_t pos_sv, int64_t pos_st, int64_t 
 
 /* ------------------------------------------------------------ batching ---
  * Batch.from_data_list for the edge_index of G graphs resident on the device
- * (SURVEY.md §8f row 2; replaces PyG's collate behind main.py:166-167 for the
+ * (replaces PyG's collate behind main.py:166-167 for the
  * packs dataset.py:77 loads onto DEVICE), fused with the batch CSR pair:
  *   out_edge_index [2, out_ld] int64: graph g's edges at columns
  *     [E_<g, E_<g + E_g), ids + N_<g (PyG __inc__);
@@ -325,7 +325,7 @@ int sldm_batch_graphs(int64_t num_graphs, const int64_t* const* edge_index,
                       int32_t* t_rowptr, int32_t* t_col, int32_t* bad_index_flag, void* stream);
 
 /* ------------------------------------------------------------------- GRU ---
- * The model's trajectory GRU (SURVEY.md §8f row 4): torch.nn.GRU(I -> H,
+ * The model's trajectory GRU: torch.nn.GRU(I -> H,
  * num_layers=1) as built at grusage.py:66-71 and called at :160-161
  * (gru_out, hlast = self.gru(x)), fp32, PyTorch's cell (aten RNN.cpp):
  *   r = s(x W_ir^T + b_ir + h W_hr^T + b_hr), z = s(... _iz ... _hz),

@@ -7,7 +7,7 @@
  * edge_index[0][e] and accumulates into row edge_index[1][e], edges visited in
  * their original order (CPU scatter_add_ order).  The product replaces that
  * per-call index_select/scatter addressing with a CSR built once per graph
- * (SURVEY.md §8a A10); this file states what that CSR must be, bit for bit:
+ *; this file states what that CSR must be, bit for bit:
  *
  *   rowptr[i]..rowptr[i+1]   in-edges of node i (dst == i)
  *   col[k]                   their sources, in original edge order (stable)

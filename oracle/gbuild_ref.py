@@ -10,7 +10,7 @@ restricted to the frames where both presence flags exceed 0.5; an edge
 same numpy / torch float32 calls as the reference, so its bits.
 
 Who may import this module: ``tests/`` only.  PARITY UNPINNED (the
-reference ships no fixtures; SURVEY.md §8c) -- this runs the reference's own
+reference ships no fixtures) -- this runs the reference's own
 numpy operations on the test inputs.
 """
 from __future__ import annotations

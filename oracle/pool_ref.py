@@ -1,7 +1,7 @@
 """ORACLE — test infrastructure only, never the product path.
 
 CPU restatement of the graph-level readout that follows the SageBlock in
-the reference (SURVEY.md §8f row 1):
+the reference:
 
 * selection: /root/reference/src/models/grusage.py:119-127
   ('mean' -> global_mean_pool, 'max' -> global_max_pool,
@@ -23,7 +23,7 @@ the reference:
   amax: the evenly split tie gradient of torch's scatter_reduce backward).
 
 Who may import this module: ``tests/`` only.  PARITY UNPINNED (no reference
-fixtures exist; SURVEY.md §8c): pinned by the hand-computed known answers in
+fixtures exist): pinned by the hand-computed known answers in
 tests/test_oracle.py.
 """
 from __future__ import annotations

@@ -8,7 +8,7 @@ activation kink in play.
 ``oracle/sage_ref.py`` runs every op in fp32, so against it a bf16 run
 differs wherever bf16 storage moves a pre-activation across the
 (Leaky)ReLU kink, and LayerNorm's backward spreads each such flip over the
-row (round 1 bounded that at 10 % relative norm).  This oracle instead keeps
+row (a norm-wise bound of ~10 % is all that comparison supports).  This oracle instead keeps
 every tensor the bf16 path *stores* in bf16 and does the arithmetic between
 the stores in fp64 (no accumulation-order noise of its own), rounding at the
 points the gfx950 kernels round:
@@ -33,7 +33,7 @@ points the gfx950 kernels round:
 With ``store=None`` (no rounding) the same code is the fp32/fp64 reference
 and must agree with ``oracle/sage_ref.py``'s autograd (tests/test_oracle.py
 pins the hand-written backward that way).  Dropout is not modelled (parity
-runs are in eval mode / dropout=None, SURVEY.md §7 (v)).
+runs are in eval mode / dropout=None).
 
 Activation-branch ties.  A pre-activation y within fp32 accumulation noise
 of the (Leaky)ReLU kink (|y| < ``ambiguity``; the GEMM's summation order

@@ -10,7 +10,7 @@ CPU restatement of the reference's SageBlock hot path, in plain PyTorch fp32
   instantiated at sageblock.py:8 and called at sageblock.py:18.  PyG is a
   third-party dependency pinned at /root/reference/uv.lock:1406-1407; it is
   absent from /root/reference and from this image, so its published
-  algorithm is restated here (SURVEY.md §8a A3-A8):
+  algorithm is restated here:
 
       x_j   = x.index_select(0, edge_index[0])                 # MessagePassing._collect
       count = zeros(N).scatter_add_(0, dst, ones(E)).clamp(min=1)
@@ -24,9 +24,8 @@ Who may import this module: ``tests/``, ``__graft_entry__.smoke()`` (as the
 checker) and ``bench.py``'s ``cpu_baseline`` leg (as the timed CPU path).  The
 product package ``sldm_sage`` never imports it.
 
-PARITY UNPINNED: the reference ships no tests, fixtures or golden vectors
- and its path cannot run here (torch_geometric is not
-installed, SURVEY.md §8c).  This restatement is cross-checked instead against
+PARITY UNPINNED: the reference ships no tests, fixtures or golden vectors and its path cannot run here (torch_geometric is not
+installed).  This restatement is cross-checked instead against
 an independent fp64 dense-matrix formulation (``oracle/dense_ref.py``) and
 hand-computed known-answer cases (``tests/test_oracle.py``).
 """
@@ -110,7 +109,7 @@ class RefSageBlock(nn.Module):
 
 
 def set_synthetic_params(block: nn.Module, seed: int = 1) -> None:
-    """Deterministic weights for parity runs (SURVEY.md §8d): lin weights and
+    """Deterministic weights for parity runs: lin weights and
     bias uniform ±1/sqrt(F_in) from ``torch.Generator().manual_seed(seed)``;
     LayerNorm weight 1, bias 0 (torch defaults).  Works on any module with the
     reference's state_dict layout."""
@@ -128,7 +127,7 @@ def set_synthetic_params(block: nn.Module, seed: int = 1) -> None:
 
 
 def random_graph(num_nodes: int, num_edges: int, feat: int, seed: int = 0):
-    """SURVEY.md §8d synthetic inputs: src, dst independent uniform
+    """Synthetic parity inputs: src, dst independent uniform
     randint(0, N, (E,)) stacked to int64 [2,E] (duplicates and self-loops
     allowed), x ~ N(0,1) [N,F] fp32, all from torch.Generator().manual_seed(seed)."""
     g = torch.Generator().manual_seed(seed)

@@ -1,4 +1,4 @@
-// Batching of per-pack graphs resident on the GPU (SURVEY.md §8f row 2): the
+// Batching of per-pack graphs resident on the GPU: the
 // edge_index half of PyG's Batch.from_data_list as the reference uses it
 // (main.py:166-167 DataLoader(batch_size=32) over packs loaded with
 // map_location=DEVICE, dataset.py:77) -- ids offset by the running node count
@@ -24,7 +24,7 @@
 // (~250 nodes, ~5k edges);
 // (1) the same without the staged pairs (steps 3 and 5 re-read edge_index);
 // (0) rows sorted in the global col / t_col slices.  Step 1 keeps kBatch
-// edges' loads in flight per thread.  r2: the global variant took 225 us per
+// edges' loads in flight per thread.  Measured: the global variant took 225 us per
 // 32-pack batch (each row's insertion sort a chain of dependent global round
 // trips), variant 1 with one load per edge per iteration 125 us.
 constexpr size_t kLdsBudget = 160 * 1024;

@@ -1,4 +1,4 @@
-// CSR build for the SageBlock hot path (SURVEY.md §8a A9/A10).
+// CSR build for the SageBlock hot path.
 //
 // edge_index [2,E] (int64 or int32, row 0 = source j, row 1 = target i; the
 // layout produced by /root/reference/src/gbuilder.py:85-112 and batched by PyG

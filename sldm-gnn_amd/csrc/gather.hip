@@ -1,4 +1,4 @@
-// CSR row gather: the SageBlock neighbour aggregation (SURVEY.md §8a A4-A5)
+// CSR row gather: the SageBlock neighbour aggregation
 // and its transpose for the backward (A8).
 //
 // Replaces, per SAGEConv call (sageblock.py:18 -> PyG 2.7.0 propagate):

@@ -1,6 +1,6 @@
 // Fused layer boundary of the SageBlock backward: the transpose gather of
 // layer l (its input gradient) straight into the LayerNorm / activation /
-// dropout backward of layer l-1 (SURVEY.md §8a A8).
+// dropout backward of layer l-1.
 //
 // Unfused, a boundary is
 //   dx_l[i]  = dx_root_l[i] + sum_{k in out(i)} g_l[t_col[k]]     gather_rows (transpose CSR)

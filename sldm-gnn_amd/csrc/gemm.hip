@@ -1,4 +1,4 @@
-// The dense part of a SageBlock layer on MFMA (SURVEY.md §8a A6, A8):
+// The dense part of a SageBlock layer on MFMA:
 //
 //   forward   h = [agg | x] · [W_l | W_r]^T            (PyG SAGEConv lin_l + lin_r)
 //             fused epilogue: + b_l, LayerNorm, LeakyReLU/ReLU, dropout (A7)

@@ -1,4 +1,4 @@
-// GRU over the vehicle trajectories (SURVEY.md §8f row 4): the model's
+// GRU over the vehicle trajectories: the model's
 // torch.nn.GRU(dynamic_features_num -> gru_hidden_size, 1 layer, batch_first)
 // (grusage.py:66-71, called at :160-161), forward and backward.
 //

@@ -1,5 +1,5 @@
 // Graph-level readout after the SageBlock: global mean / max pooling over
-// the PyG `batch` vector (SURVEY.md §8f row 1).
+// the PyG `batch` vector.
 //
 // Replaces (grusage.py:119-127, :185): PyG 2.7.0 global_mean_pool(x, batch)
 // = utils.scatter(x, batch, reduce='mean') and global_max_pool(x, batch) =

@@ -1,6 +1,6 @@
-// Post-conv elementwise stage of a SageBlock layer (SURVEY.md §8a A6 epilogue +
-// A7): lin_l bias -> LayerNorm(F_out, eps) -> LeakyReLU(ns)/ReLU -> Dropout(p),
-// /root/reference/src/models/blocks/sageblock.py:9-15, and its backward (A8).
+// Post-conv elementwise stage of a SageBlock layer:
+// lin_l bias -> LayerNorm(F_out, eps) -> LeakyReLU(ns)/ReLU -> Dropout(p),
+// /root/reference/src/models/blocks/sageblock.py:9-15, and its backward.
 //
 // Row-wise and HBM-bound: a row is owned by LPR lanes (power of two <= 64),
 // each holding NCH x V consecutive features in registers, so the LayerNorm

@@ -1,5 +1,4 @@
-// Trajectory-radius edge construction of the vehicle graph (SURVEY.md §8f
-// row 3): the O(V^2 T) pair loop of the reference's graph builders, on the GPU.
+// Trajectory-radius edge construction of the vehicle graph: the O(V^2 T) pair loop of the reference's graph builders, on the GPU.
 //
 // Replaces gbuilder.py:85-111 (offline builder) and :241-268
 // (GraphOnlineCreator, the latency path of rcv.py:77):

@@ -1,6 +1,6 @@
 // A non-Python host of libsldm_sage.so: the C ABI (include/sldm_sage.h) driven
 // from plain C++ with the HIP runtime -- what a host in another language binds
-// through its FFI (INTEGRATION.md section 3).  Builds the CSR of a random graph
+// through its FFI.  Builds the CSR of a random graph
 // on the GPU, runs the mean aggregation (the reference's index_select +
 // scatter-mean, sageblock.py:18) and its transpose-gather backward, and checks
 // both bit for bit against a host restatement of the reference's order (fp32

@@ -1,6 +1,6 @@
 """sldm_sage — MI355X-native (gfx950) SageBlock hot path of aledima00/sldm-gnn.
 
-Drop-in for ``src/models/blocks/sageblock.py`` (see INTEGRATION.md):
+Drop-in for ``src/models/blocks/sageblock.py``:
 
     from sldm_sage import SageBlock
 

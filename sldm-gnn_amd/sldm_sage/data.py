@@ -1,5 +1,5 @@
 """PyG-free batching of the reference's graphs, emitting the SageBlock CSR at
-collate time (SURVEY.md §8f row 2).
+collate time.
 
 Replaces ``torch_geometric.loader.DataLoader`` / ``Batch.from_data_list``
 as used by the reference (main.py:3, :166-167; test.py:9; utils.py:2, :218,

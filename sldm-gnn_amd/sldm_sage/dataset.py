@@ -1,4 +1,4 @@
-"""PyG-free ingest of the reference's ``pack_*.pt`` graphs (SURVEY.md §8f row 2).
+"""PyG-free ingest of the reference's ``pack_*.pt`` graphs.
 
 The reference loads each pack with ``torch.load(path, map_location=device)``
 under ``safe_globals([DataEdgeAttr, DataTensorAttr, GlobalStorage])``

@@ -1,4 +1,4 @@
-"""The dense part of a SAGEConv layer (SURVEY.md §8a A6) on hand-written MFMA
+"""The dense part of a SAGEConv layer on hand-written MFMA
 kernels: one contraction [agg | x] · [W_l | W_r]^T per layer with the bias,
 LayerNorm, activation and dropout fused in its epilogue, and the two backward
 contractions (input grads with the 1/deg prescale fused; weight grads split

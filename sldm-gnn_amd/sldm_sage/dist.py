@@ -1,7 +1,6 @@
 """Multi-GPU SageBlock: destination-row partition + RCCL halo exchange.
 
-No reference counterpart (the reference has no distributed code, SURVEY.md
-§2, §8e): a full-graph SageBlock forward/backward shards naturally by
+No reference counterpart (the reference has no distributed code): a full-graph SageBlock forward/backward shards naturally by
 destination node because the mean aggregation of row i reads only i's
 in-edges, and the dense part, LayerNorm and activation are row-local.
 
@@ -201,7 +200,7 @@ def broadcast(t: torch.Tensor, src: int = 0, group=None) -> None:
 # Row blocks.  Rank r owns the contiguous node rows [bounds[r], bounds[r+1]).
 # "rows": equal row counts (P = ceil(N/W)); "cost": cut by the cumulative
 # per-node cost (in-degree + out-degree + the dense part's row cost in
-# edge-equivalents), SURVEY.md §8e's "split by cumulative in-degree" for
+# edge-equivalents), a split by cumulative in-degree for
 # power-law graphs -- a 10k-in-degree hub then weighs as much as ~10k rows'
 # edges instead of one row.
 # ---------------------------------------------------------------------------
@@ -910,7 +909,7 @@ class DistSageBlock(nn.Module):
 # ---------------------------------------------------------------------------
 # Strategy planner
 # ---------------------------------------------------------------------------
-# Cost-model constants (MI355X, measured on one GPU; see DESIGN.md §6):
+# Cost-model constants (MI355X, measured on one GPU):
 #   gather rate by gathered row width, uniform random rows of a multi-GB
 #   table (tools/gather_probe.py, profiles/r1_gather_probe.txt);
 #   xGMI: one link per peer, ~50 GB/s achieved per direction (conservative
@@ -934,7 +933,7 @@ def _remote_unique(ids: torch.Tensor, r0: int, r1: int) -> int:
 
 
 # dense part (fwd GEMM + LN, LN backward, dX, dW) per layer and row, in units
-# of F*s bytes at the stream kernels' measured rate (§4: ~13 F s per row)
+# of F*s bytes at the stream kernels' measured rate (~13 F s per row)
 _DENSE_BYTES_PER_ROW_FS = 13.0
 _DENSE_BPS = 4.0e12
 _FEAT_CHUNKS = 4          # partition_features' default pipeline depth

@@ -1,4 +1,4 @@
-"""Vehicle-graph edge construction on the GPU (SURVEY.md §8f row 3).
+"""Vehicle-graph edge construction on the GPU.
 
 ``radius_edges(pos, presence, radius)`` replaces the O(V^2 T) Python pair
 loop of the reference's graph builders -- gbuilder.py:85-111 (offline,

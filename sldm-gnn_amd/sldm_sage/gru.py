@@ -1,4 +1,4 @@
-"""Drop-in ``GRU`` for the model's trajectory encoder (SURVEY.md §8f row 4).
+"""Drop-in ``GRU`` for the model's trajectory encoder.
 
 GruSage builds ``torch.nn.GRU(input_size=dynamic_features_num,
 hidden_size=gru_hidden_size, num_layers=gru_num_layers, batch_first=True)``

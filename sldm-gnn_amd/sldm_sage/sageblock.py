@@ -20,7 +20,7 @@ stack as sage_stack_fwd / sage_stack_bwd) over the C ABI:
   backward: LN/act/dropout bwd -> dh·[W_l|W_r] -> dW -> 1/deg prescale ->
             transpose gather + lin_r grad
 Dropout masks come from a counter-based hash (not torch's RNG stream), so
-parity runs use eval mode or dropout=None (SURVEY.md §7 (v)).
+parity runs use eval mode or dropout=None.
 """
 from __future__ import annotations
 

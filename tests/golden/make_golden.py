@@ -6,7 +6,7 @@ Each .npz holds inputs (edge_index, x, upstream gradient gout, the SageBlock
 state_dict as ``sd.<key>``, hdims, negative_slope) and the oracle's outputs
 (out, dx, ``grad.<param>``), fp32, eval mode / dropout None.  The oracle is
 oracle/sage_ref.py (plain-torch restatement of PyG 2.7.0 SAGEConv + the
-reference SageBlock); parity is unpinned by reference outputs (DESIGN.md).
+reference SageBlock); parity is unpinned by reference outputs.
 Seeds are fixed, so re-running reproduces the files bit for bit.
 """
 from __future__ import annotations

@@ -1,4 +1,4 @@
-"""PyG-free collate (SURVEY.md §8f row 2): Batch.from_data_list semantics for
+"""PyG-free collate: Batch.from_data_list semantics for
 the reference's graph records and the batch CSR emitted at collate time.
 
 CPU: attribute concatenation / offsets / batch / ptr against an independent

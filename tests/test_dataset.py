@@ -1,6 +1,6 @@
-"""PyG-free ``.pt`` ingest (sldm_sage.dataset, SURVEY.md §8f row 2) on CPU.
+"""PyG-free ``.pt`` ingest (sldm_sage.dataset) on CPU.
 
-torch_geometric is not installed here (SURVEY.md §8c), so the pickles are
+torch_geometric is not installed here, so the pickles are
 written with stand-in classes registered under PyG's module paths, shaped
 like PyG 2.x's ``Data`` / ``GlobalStorage`` pickle state (a ``_store``
 storage holding the attribute ``_mapping`` and a back-reference to its
@@ -181,7 +181,7 @@ def test_ingest_feeds_collate(pack_dir):
 
 
 def test_collate_csr_cache_follows_edge_index():
-    """the per-graph host CSR is keyed on the edge_index tensor and
+    """The per-graph host CSR is keyed on the edge_index tensor and
     its version, so an in-place rewire with the same edge count is seen."""
     from sldm_sage.data import collate, host_csr
     from sldm_sage.dataset import PackGraph

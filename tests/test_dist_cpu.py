@@ -153,7 +153,7 @@ def test_dist_sageblock_dropout_on_cpu_tensors(strategy, train):
 
 
 def test_halo_closed_component_rank_joins_exchange():
-    """a rank whose block exchanges nothing must still take part in
+    """A rank whose block exchanges nothing must still take part in
     the halo all-to-alls the other ranks issue (global skip decision)."""
     _run(3, 300, [8, 12, 8], "halo", graph="closed1", balance="rows")
 

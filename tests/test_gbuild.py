@@ -1,4 +1,4 @@
-"""Radius-edge construction (SURVEY.md §8f row 3): the GPU kernel against
+"""Radius-edge construction: the GPU kernel against
 the reference's numpy pair loop (oracle/gbuild_ref.py), bit for bit: same
 edges in the same order, same float32 edge attributes.
 

@@ -436,8 +436,8 @@ def test_sageblock_fwd_bwd(n, e, hdims, ns, dtype):
 def test_sageblock_bf16_kinked_elementwise(hdims, ns):
     """bf16 with the activation kink in play and a non-trivial LayerNorm
     affine (random gamma / beta): forward and every gradient element-wise
-    within 1e-2 of the bf16-storage oracle (round 1 held gradients only to
-    10 % relative norm against the fp32 oracle)."""
+    within 1e-2 of the bf16-storage oracle (against the fp32 oracle the gradients hold only a
+    ~10 % relative-norm bound)."""
     from sldm_sage import SageBlock
     from oracle.sage_bf16_ref import block_params, branch_margin
     from oracle.sage_ref import random_graph
@@ -1226,7 +1226,7 @@ def test_full_size_c5_powerlaw_khop_parity(dtype):
 
 
 def test_dropout_seeds_leave_cpu_rng_untouched():
-    """ADVICE r1: SageBlock's dropout keys come from the device generator
+    """SageBlock's dropout keys come from the device generator
     (like nn.Dropout on a GPU), not torch's global CPU generator: the caller's
     CPU RNG stream is unchanged by a training forward, torch.manual_seed still
     reproduces the masks, and successive calls draw new masks."""

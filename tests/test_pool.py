@@ -1,4 +1,4 @@
-"""Graph-level readout (SURVEY.md §8f row 1): global mean / max / mean||max
+"""Graph-level readout: global mean / max / mean||max
 pooling over the batch vector.
 
 CPU: the oracle (oracle/pool_ref.py, PyG 2.7.0's CPU op sequence) against
