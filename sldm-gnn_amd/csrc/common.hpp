@@ -364,6 +364,25 @@ int stream_dense_fwd(const void* a0, int64_t lda0, int64_t k0, const void* a1, i
 int stream_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int64_t ldb,
                          int64_t num_rows, int64_t nc, const int32_t* rowptr, int64_t scale_cols,
                          void* out, int64_t ldo, void* out2, int64_t ldo2, hipStream_t stream);
+// Persistent fp32 kernels on six-term split-bf16 products (gemm_stream_f32.hip):
+// the forward at F_out = 256 and the dX GEMM at 256 | 512 output columns, K in
+// {256, 512}.  SLDM_STREAM_F32=0 disables them (the 64-row tile kernels run).
+bool stream_f32_enabled();
+bool stream_f32_dense_fwd_ok(int64_t k0, int64_t K, int64_t nc, const void* a0, int64_t lda0,
+                             const void* a1, int64_t lda1, const void* w, const void* out,
+                             const void* xhat);
+bool stream_f32_rowscale_ok(int64_t k, int64_t nc, const void* a, int64_t lda, const void* b,
+                            int64_t ldb, const void* out, int64_t ldo, const void* out2,
+                            int64_t ldo2, int64_t scale_cols);
+int stream_f32_dense_fwd(const void* a0, int64_t lda0, int64_t k0, const void* a1, int64_t lda1,
+                         int64_t k1, const void* w, int64_t num_rows, const float* bias,
+                         const float* gamma, const float* beta, float eps, float slope,
+                         float drop_p, uint64_t seed, int64_t row_off, void* out, void* xhat,
+                         float* rstd, hipStream_t stream);
+int stream_f32_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int64_t ldb,
+                             int64_t num_rows, int64_t nc, const int32_t* rowptr,
+                             int64_t scale_cols, void* out, int64_t ldo, void* out2, int64_t ldo2,
+                             hipStream_t stream);
 // gemm_ws.hip: weight-stationary dX kernel (weights in VGPRs, LDS-DMA tiles).
 bool ws_gemm_enabled();
 // gemm_tn_dma.hip: row-streaming dW kernel (LDS-DMA, transposed reads).

@@ -1195,6 +1195,12 @@ extern "C" int sldm_sage_dense_fwd(int dtype, const void* a0, int64_t lda0, int6
     return sldm::big_dense_fwd(a0, lda0, k0, a1, lda1, k1, w, num_rows, nc, bias, gamma, beta,
                                eps, negative_slope, drop_p, seed, row_off, out, xhat, rstd,
                                stream);
+  if (dtype == SLDM_F32 && sldm::fp32_gemm_split() && sldm::stream_f32_enabled() &&
+      sldm::stream_f32_dense_fwd_ok(k0, k0 + k1, nc, a0, lda0, k1 ? a1 : a0, k1 ? lda1 : lda0, w,
+                                    out, xhat))
+    return sldm::stream_f32_dense_fwd(a0, lda0, k0, a1, lda1, k1, w, num_rows, bias, gamma, beta,
+                                      eps, negative_slope, drop_p, seed, row_off, out, xhat, rstd,
+                                      stream);
   auto fill = [&](auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
     NtArgs<T> p{};
@@ -1250,6 +1256,11 @@ extern "C" int sldm_gemm_nt_rowscale(int dtype, const void* a, int64_t lda, int6
       return sldm::big_gemm_rowscale(a, lda, k, b, ldb, num_rows, nc, bn, rowptr, scale_cols,
                                      out, ldo, out2, ldo2, stream);
   }
+  if (dtype == SLDM_F32 && sldm::fp32_gemm_split() && sldm::stream_f32_enabled() &&
+      sldm::stream_f32_rowscale_ok(k, nc, a, lda, b, ldb, out, ldo, out2, ldo2,
+                                   rowptr || out2 ? scale_cols : 0))
+    return sldm::stream_f32_gemm_rowscale(a, lda, k, b, ldb, num_rows, nc, rowptr, scale_cols,
+                                          out, ldo, out2, ldo2, stream);
   auto fill = [&](auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
     NtArgs<T> p{};
@@ -1365,8 +1376,8 @@ extern "C" int sldm_gemm_tn_split(int dtype, const void* a, int64_t lda, int64_t
 }
 
 namespace sldm {
-// fp32 dense GEMMs run as split-bf16 products (hi.hi + hi.lo + lo.hi on the
-// bf16 MFMA, ~2^-16 relative per product, fp32 accumulation) wherever a
+// fp32 dense GEMMs run as six-term split-bf16 products (three-way operand
+// split on the bf16 MFMA, fp32-level products, fp32 accumulation) wherever a
 // kernel has that form; SLDM_FP32_GEMM=exact selects the exact fp32 MFMA
 // (v_mfma_f32_16x16x4_f32, 1/16 of the bf16 rate) everywhere.  Read per call
 // so tests can compare both forms in one process.

@@ -907,6 +907,87 @@ def test_fp32_ws32_nt_bit_exact_vs_tile(m, f, monkeypatch):
         torch.testing.assert_close(a, c, atol=1e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("m", STREAM_ROWS + [63, 65])
+@pytest.mark.parametrize("fi", [128, 256])
+def test_fp32_stream_dense_fwd_vs_fp64_and_tile(m, fi, monkeypatch):
+    """gemm_stream_f32.hip, forward (fp32 at F_out = 256, K = 2 fi:
+    persistent 256-row tiles, six-term split-bf16 products, LayerNorm +
+    LeakyReLU + dropout epilogue) against an fp64 reference at the fp32 bar,
+    against the 64-row tile kernel (SLDM_STREAM_F32=0) at fp32 rounding noise,
+    and the same dropout mask; without saved statistics too."""
+    from sldm_sage import ops
+    fo, p, seed = 256, 0.25, 77
+    gen = torch.Generator(device=DEV).manual_seed(3 * m + fi)
+    agg = torch.randn(m, fi, generator=gen, device=DEV)
+    x = torch.randn(m, fi, generator=gen, device=DEV)
+    k = 2 * fi
+    wcat = torch.randn(fo, k, generator=gen, device=DEV) / k ** 0.5
+    bl, gam = (torch.randn(fo, generator=gen, device=DEV) for _ in range(2))
+    bet = torch.full((fo,), 6.0, device=DEV)            # y != 0: the kept mask is out != 0
+
+    def run(stream, save=True):
+        monkeypatch.setenv("SLDM_STREAM_F32", "1" if stream else "0")
+        r = ops.sage_dense_fwd(agg, x, wcat, bl, gam, bet, 1e-5, 0.1, p, seed, save)
+        torch.cuda.synchronize()
+        return r
+
+    out, xhat, rstd = run(True)
+    h = torch.cat([agg, x], 1).double() @ wcat.double().t() + bl.double()
+    mu = h.mean(1, keepdim=True)
+    rs = 1 / torch.sqrt(((h - mu) ** 2).mean(1, keepdim=True) + 1e-5)
+    xh = (h - mu) * rs
+    y = xh * gam.double() + bet.double()
+    z = torch.where(y > 0, y, 0.1 * y) / (1 - p)
+    kept = out != 0
+    torch.testing.assert_close(out.double()[kept], z[kept], atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(xhat.double(), xh, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(rstd.double(), rs.squeeze(1), atol=1e-5, rtol=1e-5)
+    t_out, t_xhat, t_rstd = run(False)
+    assert torch.equal(kept, t_out != 0)
+    torch.testing.assert_close(out, t_out, atol=2e-5, rtol=1e-5)
+    torch.testing.assert_close(xhat, t_xhat, atol=2e-5, rtol=1e-5)
+    torch.testing.assert_close(rstd, t_rstd, atol=1e-6, rtol=1e-5)
+    # the activation branch and the mask post_bwd recomputes from the saved xhat
+    y_dev = torch.addcmul(bet, xhat, gam)
+    assert torch.equal((out > 0)[kept], (y_dev > 0)[kept])
+    o2, x2, r2 = run(True, save=False)
+    assert x2 is None and r2 is None and torch.equal(o2, out)
+
+
+@pytest.mark.parametrize("m", STREAM_ROWS + [63, 65, 40_000])
+@pytest.mark.parametrize("k,nc", [(256, 512), (256, 256), (512, 512)])
+def test_fp32_stream_gemm_rowscale_vs_fp64_and_tile(m, k, nc, monkeypatch):
+    """gemm_stream_f32.hip, dX: dZ [W_l | W_r] with the first half divided by
+    the in-degree; 512 output columns run as two column halves on workgroup
+    pairs.  One buffer and split outputs, with and without the degree scale,
+    against fp64 and the tile kernel; the division is the tile kernel's, so
+    scaled and unscaled entries agree to fp32 summation-order noise."""
+    from sldm_sage import build_graph, ops
+    from oracle.sage_ref import random_graph
+    fi = nc // 2
+    ei, _ = random_graph(m, 3 * m + 1, 1, seed=m + k)
+    g = build_graph(ei.to(DEV), m)
+    gen = torch.Generator(device=DEV).manual_seed(m + k + nc)
+    dh = torch.randn(m, k, generator=gen, device=DEV)
+    wt = torch.randn(nc, k, generator=gen, device=DEV) / k ** 0.5
+
+    def run(stream, rowptr, split):
+        monkeypatch.setenv("SLDM_STREAM_F32", "1" if stream else "0")
+        r = ops.gemm_nt_rowscale(dh, wt, rowptr, fi, split=split)
+        torch.cuda.synchronize()
+        return torch.cat(r, 1) if split else r
+
+    for rowptr in (g.rowptr, None):
+        got = run(True, rowptr, False)
+        ref = dh.double() @ wt.double().t()
+        if rowptr is not None:
+            ref[:, :fi] /= (rowptr[1:] - rowptr[:-1]).clamp(min=1).double()[:, None]
+        torch.testing.assert_close(got.double(), ref, atol=1e-4, rtol=1e-4)
+        torch.testing.assert_close(got, run(False, rowptr, False), atol=2e-5, rtol=1e-5)
+        if fi % 256 == 0:
+            assert torch.equal(run(True, rowptr, True), got)
+
+
 # ------------------------------------------------ overlapped (split) gather --
 @pytest.mark.parametrize("mean", [True, False])
 def test_overlapped_gather_split_is_bit_exact(mean):
