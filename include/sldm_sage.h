@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SLDM_ABI_VERSION 7   /* 7: + sldm_gather_rows_split_static */
+#define SLDM_ABI_VERSION 8   /* 8: + sldm_gemm_nt_rowscale_blocked(_ok) */
 
 enum sldm_dtype { SLDM_F32 = 0, SLDM_BF16 = 1 };
 enum sldm_status { SLDM_OK = 0, SLDM_ERR_ARG = 1, SLDM_ERR_HIP = 2 };
@@ -196,6 +196,24 @@ int sldm_gemm_nt_rowscale(int dtype, const void* a, int64_t lda, int64_t k,
                           const void* b, int64_t ldb, int64_t num_rows, int64_t nc,
                           const int32_t* rowptr, int64_t scale_cols,
                           void* out, int64_t ldo, void* out2, int64_t ldo2, void* stream);
+
+/* The same product with the degree-scaled half written column-blocked:
+ * out_blocked is [scale_cols / blk_cols] blocks of [num_rows][blk_cols]
+ * (block j = columns [j blk_cols, (j+1) blk_cols) of every row, contiguous),
+ * the unscaled half goes to out2 [num_rows, nc - scale_cols] as above.  This
+ * is the send layout of the all-to-all that turns a rank's row block into
+ * every rank's column slice (feature-sliced partitions), written by the GEMM
+ * instead of by a packing copy.  No reference counterpart (the reference has
+ * no distributed code).  Shapes: ask sldm_gemm_nt_rowscale_blocked_ok (1 = the
+ * call is supported; others return SLDM_ERR_ARG); values are bit-identical to
+ * sldm_gemm_nt_rowscale's. */
+int sldm_gemm_nt_rowscale_blocked_ok(int dtype, int64_t k, int64_t nc, int64_t scale_cols,
+                                     int64_t blk_cols);
+int sldm_gemm_nt_rowscale_blocked(int dtype, const void* a, int64_t lda, int64_t k,
+                                  const void* b, int64_t ldb, int64_t num_rows, int64_t nc,
+                                  const int32_t* rowptr, int64_t scale_cols,
+                                  void* out_blocked, int64_t blk_cols, void* out2, int64_t ldo2,
+                                  void* stream);
 
 /* out[mo, n0+n1] (fp32) = sum_{r < num_rows} a[r, :]^T ⊗ [b0 | b1][r, :]
  * Weight gradients [dW_l | dW_r] = dh^T · [agg | x] (A8), split over the

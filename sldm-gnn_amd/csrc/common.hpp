@@ -395,9 +395,12 @@ int tn_dma(const void* a, int64_t lda, const void* b0, int64_t ldb0, const void*
 bool ws_rowscale_ok(int64_t k, int64_t nc, int64_t num_rows, const void* a, int64_t lda,
                     const void* b, int64_t ldb, const void* out, int64_t ldo, const void* out2,
                     int64_t ldo2, int64_t scale_cols);
+// blk_shift > 0: the scaled half goes to ``out`` as [scale_cols >> blk_shift]
+// blocks of [num_rows][1 << blk_shift] (out2 required, ldo ignored).
 int ws_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int64_t ldb,
                      int64_t num_rows, int64_t nc, const int32_t* rowptr, int64_t scale_cols,
-                     void* out, int64_t ldo, void* out2, int64_t ldo2, hipStream_t stream);
+                     void* out, int64_t ldo, void* out2, int64_t ldo2, hipStream_t stream,
+                     int blk_shift = 0);
 }  // namespace sldm
 
 #define SLDM_REQUIRE(cond, ...)          \

@@ -1128,7 +1128,8 @@ struct TnPlan {
   int64_t chunk;
 };
 
-TnPlan tn_plan(int64_t rows, int64_t mo, int64_t nn) {
+// ``x6``: the plan of the fp32 split-bf16 kernel (two resident blocks per CU).
+TnPlan tn_plan(int64_t rows, int64_t mo, int64_t nn, bool x6 = false) {
   TnPlan pl;
   pl.tiles_m = (int)((mo + TN_TILE - 1) / TN_TILE);
   pl.tiles_n = (int)((nn + TN_TILE - 1) / TN_TILE);
@@ -1142,7 +1143,9 @@ TnPlan tn_plan(int64_t rows, int64_t mo, int64_t nn) {
   }();
   // 768 measured best at C4 (10M rows: 4.63 -> 3.84 ms vs 512); short node
   // dimensions keep 512 (C2: the extra slabs cost more than they hide)
-  int64_t splits = (target ? target : (rows >= 2000000 ? 768 : 512)) / tiles;
+  // the split-bf16 fp32 kernel holds six LDS images (two blocks per CU): 1024
+  // blocks = two full rounds (C4 dW 16.9 -> 15.5 ms against 768)
+  int64_t splits = (target ? target : (rows >= 2000000 ? (x6 ? 1024 : 768) : 512)) / tiles;
   // >= 8 k-steps per split on long node dimensions; short ones (the vehicle
   // batches' ~8k rows: 31 splits = 48 blocks of 11 k-steps, 40 us of mostly
   // idle CUs) take more, shorter splits; SLDM_TN_MINK overrides (A/B runs)
@@ -1277,10 +1280,40 @@ extern "C" int sldm_gemm_nt_rowscale(int dtype, const void* a, int64_t lda, int6
   return dtype == SLDM_F32 ? fill((float*)nullptr) : fill((uint16_t*)nullptr);
 }
 
+extern "C" int sldm_gemm_nt_rowscale_blocked_ok(int dtype, int64_t k, int64_t nc,
+                                                int64_t scale_cols, int64_t blk_cols) {
+  return dtype == SLDM_BF16 && sldm::ws_gemm_enabled() && k == 256 && nc == 512 &&
+         scale_cols == 256 && (blk_cols == 32 || blk_cols == 64 || blk_cols == 128);
+}
+
+extern "C" int sldm_gemm_nt_rowscale_blocked(int dtype, const void* a, int64_t lda, int64_t k,
+                                             const void* b, int64_t ldb, int64_t num_rows,
+                                             int64_t nc, const int32_t* rowptr,
+                                             int64_t scale_cols, void* out_blocked,
+                                             int64_t blk_cols, void* out2, int64_t ldo2,
+                                             void* stream_) {
+  SLDM_REQUIRE(sldm_gemm_nt_rowscale_blocked_ok(dtype, k, nc, scale_cols, blk_cols),
+               "sldm_gemm_nt_rowscale_blocked: unsupported shape (dtype %d k %lld nc %lld "
+               "scale_cols %lld blk_cols %lld); ask sldm_gemm_nt_rowscale_blocked_ok first",
+               dtype, (long long)k, (long long)nc, (long long)scale_cols, (long long)blk_cols);
+  SLDM_REQUIRE(num_rows >= 0 && lda >= k && ldb >= k && ldo2 >= nc - scale_cols,
+               "sldm_gemm_nt_rowscale_blocked: bad sizes");
+  if (num_rows == 0) return SLDM_OK;
+  SLDM_REQUIRE(a && b && out_blocked && out2, "sldm_gemm_nt_rowscale_blocked: NULL argument");
+  SLDM_REQUIRE(sldm::ws_rowscale_ok(k, nc, num_rows, a, lda, b, ldb, out_blocked, blk_cols, out2,
+                                    ldo2, scale_cols),
+               "sldm_gemm_nt_rowscale_blocked: operands must be 16-byte aligned with row "
+               "strides that are multiples of 8 elements");
+  const int sh = blk_cols == 32 ? 5 : (blk_cols == 64 ? 6 : 7);
+  return sldm::ws_gemm_rowscale(a, lda, k, b, ldb, num_rows, nc, rowptr, scale_cols, out_blocked,
+                                blk_cols, out2, ldo2, sldm::as_stream(stream_), sh);
+}
+
 extern "C" size_t sldm_gemm_tn_workspace_bytes(int64_t num_rows, int64_t mo, int64_t nn) {
   if (num_rows <= 0 || mo <= 0 || nn <= 0) return 16;
-  TnPlan pl = tn_plan(num_rows, mo, nn);
-  size_t need = sizeof(float) * (size_t)pl.splits * (size_t)mo * (size_t)nn + 256;
+  // no dtype here: room for the larger of the two plans
+  const int splits = std::max(tn_plan(num_rows, mo, nn).splits, tn_plan(num_rows, mo, nn, true).splits);
+  size_t need = sizeof(float) * (size_t)splits * (size_t)mo * (size_t)nn + 256;
   if (mo == 256 && (nn == 256 || nn == 512))   // gemm_tn_dma.hip's slab may be larger
     need = std::max(need, sldm::tn_dma_workspace_bytes(num_rows, nn));
   return need;
@@ -1320,27 +1353,24 @@ int gemm_tn_impl(int dtype, const void* a, int64_t lda, int64_t mo, const void* 
     SLDM_LAUNCH_CHECK("slab_reduce_kernel");
     return SLDM_OK;
   }
-  TnPlan pl = tn_plan(num_rows, mo, nn);
   auto run = [&](auto* tag) -> int {
     using T = std::remove_pointer_t<decltype(tag)>;
     constexpr int EPV = 16 / sizeof(T);
+    auto al = [](const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; };
+    const bool vec = (mo % EPV == 0) && (n0 % EPV == 0) && (n1 % EPV == 0) && (lda % EPV == 0) &&
+                     (ldb0 % EPV == 0) && (n1 == 0 || ldb1 % EPV == 0) && al(a) && al(b0) &&
+                     (n1 == 0 || al(b1));
+    const bool x6 = sizeof(T) == 4 && vec && sldm::fp32_gemm_split();
+    const TnPlan pl = tn_plan(num_rows, mo, nn, x6);
     TnArgs<T> p{};
     p.a = (const T*)a; p.lda = lda; p.mo = (int)mo;
     p.b0 = (const T*)b0; p.ldb0 = ldb0; p.n0 = (int)n0;
     p.b1 = n1 ? (const T*)b1 : (const T*)b0; p.ldb1 = n1 ? ldb1 : ldb0; p.nn = (int)nn;
     p.rows = num_rows; p.chunk = pl.chunk; p.splits = pl.splits;
     p.tiles_m = pl.tiles_m; p.tiles_n = pl.tiles_n; p.slab = slab;
-    auto al = [](const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; };
-    const bool vec = (mo % EPV == 0) && (n0 % EPV == 0) && (n1 % EPV == 0) && (lda % EPV == 0) &&
-                     (ldb0 % EPV == 0) && (n1 == 0 || ldb1 % EPV == 0) && al(a) && al(b0) &&
-                     (n1 == 0 || al(b1));
     const unsigned grid = (unsigned)(pl.splits * pl.tiles_m * pl.tiles_n);
-    bool x6 = false;
     if constexpr (sizeof(T) == 4) {
-      if (vec && sldm::fp32_gemm_split()) {
-        gemm_tn_x6_kernel<<<grid, kBlock, 0, stream>>>(p);
-        x6 = true;
-      }
+      if (x6) gemm_tn_x6_kernel<<<grid, kBlock, 0, stream>>>(p);
     }
     if (x6) {
     } else if (vec)

@@ -49,6 +49,7 @@ struct WsArgs {
   uint16_t* out; int64_t ldo;
   uint16_t* out2; int64_t ldo2;       // optional home of columns >= scale_cols
   const int32_t* rowptr; int scale_cols;
+  int blk_shift;                      // > 0: ``out`` is [scale_cols >> blk_shift][M][1 << blk_shift]
 };
 
 template <int N>
@@ -144,6 +145,11 @@ __global__ __launch_bounds__(kThreads) void ws_rowscale_kernel(WsArgs p) {
   uint16_t* obase = p.out;
   int64_t ldo = p.ldo;
   if (p.out2 && cbase >= p.scale_cols) { obase = p.out2 - p.scale_cols; ldo = p.ldo2; }
+  // column-blocked home of the scaled half (the send layout of a feature-
+  // sliced partition's all-to-all): block c >> sh holds columns [c, c + 2^sh)
+  // of every row, contiguous; a lane's 8 columns never straddle a block
+  const int sh = p.blk_shift;
+  const bool blocked = sh > 0 && cbase < p.scale_cols;
 
   for (int64_t n = 0;; ++n) {
     const int64_t tile = blockIdx.x + n * grid;
@@ -221,8 +227,12 @@ __global__ __launch_bounds__(kThreads) void ws_rowscale_kernel(WsArgs p) {
         }
         auto s0 = __builtin_amdgcn_permlane16_swap(w[0][0], w[1][0], false, false);
         auto s1 = __builtin_amdgcn_permlane16_swap(w[0][1], w[1][1], false, false);
-        *reinterpret_cast<uint4*>(obase + row * ldo + ccol + 16 * t) =
-            make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        uint16_t* dst = obase + row * ldo + ccol + 16 * t;
+        if (blocked) {
+          const int c = ccol + 16 * t;
+          dst = p.out + ((((int64_t)(c >> sh)) * p.M + row) << sh) + (c & ((1 << sh) - 1));
+        }
+        *reinterpret_cast<uint4*>(dst) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
       }
     }
   }
@@ -283,9 +293,11 @@ bool ws_rowscale_ok(int64_t k, int64_t nc, int64_t num_rows, const void* a, int6
 
 int ws_gemm_rowscale(const void* a, int64_t lda, int64_t k, const void* b, int64_t ldb,
                      int64_t num_rows, int64_t nc, const int32_t* rowptr, int64_t scale_cols,
-                     void* out, int64_t ldo, void* out2, int64_t ldo2, hipStream_t stream) {
+                     void* out, int64_t ldo, void* out2, int64_t ldo2, hipStream_t stream,
+                     int blk_shift) {
   (void)k;
   WsArgs p{};
+  p.blk_shift = blk_shift;
   p.a = (const uint16_t*)a; p.lda = lda;
   p.b = (const uint16_t*)b; p.ldb = ldb;
   p.M = num_rows;

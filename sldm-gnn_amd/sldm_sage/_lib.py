@@ -15,7 +15,7 @@ import torch  # noqa: F401  (must be imported before the HIP library)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SLDM_SAGE_LIB", os.path.join(_HERE, "libsldm_sage.so"))
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 F32, BF16 = 0, 1
 
 _c_i64 = ctypes.c_int64
@@ -61,6 +61,11 @@ _SIGNATURES = {
     "sldm_gemm_nt_rowscale": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _c_i64, _vp, _c_i64,
                                              _c_i64, _c_i64, _vp, _c_i64, _vp, _c_i64, _vp,
                                              _c_i64, _vp]),
+    "sldm_gemm_nt_rowscale_blocked_ok": (ctypes.c_int, [ctypes.c_int, _c_i64, _c_i64, _c_i64,
+                                                        _c_i64]),
+    "sldm_gemm_nt_rowscale_blocked": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _c_i64, _vp,
+                                                     _c_i64, _c_i64, _c_i64, _vp, _c_i64, _vp,
+                                                     _c_i64, _vp, _c_i64, _vp]),
     "sldm_gemm_tn_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, _c_i64]),
     "sldm_gemm_tn": (ctypes.c_int, [ctypes.c_int, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64,
                                     _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, ctypes.c_size_t,

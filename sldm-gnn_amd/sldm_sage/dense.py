@@ -44,6 +44,20 @@ def sage_linear_bwd_data(dh: torch.Tensor, wl: torch.Tensor, wr: torch.Tensor,
     return buf[:, :fi], buf[:, fi:]
 
 
+def sage_linear_bwd_data_blocked_ok(dh: torch.Tensor, fi: int, blk_cols: int) -> bool:
+    return ops.gemm_nt_rowscale_blocked_ok(dh, 2 * fi, fi, blk_cols)
+
+
+def sage_linear_bwd_data_blocked(dh: torch.Tensor, wcat_t: torch.Tensor, rowptr: torch.Tensor,
+                                 fi: int, blk_cols: int, dx_root: torch.Tensor):
+    """:func:`sage_linear_bwd_data` with dAgg / deg returned column-blocked
+    (flat [fi // blk_cols][N][blk_cols], the send layout of a feature-sliced
+    partition) and the root-path grad written into ``dx_root`` [N, F_in].
+    ``wcat_t``: [W_l | W_r]^T, [2 F_in, F_out] contiguous."""
+    blocked, _ = ops.gemm_nt_rowscale_blocked(dh, wcat_t, rowptr, fi, blk_cols, out2=dx_root)
+    return blocked
+
+
 def sage_linear_bwd_weight(dh: torch.Tensor, agg: torch.Tensor, x: torch.Tensor):
     """(dW_l, dW_r) = (dh^T · agg, dh^T · x), fp32, one launch + its reduce
     writing both (no slicing copies)."""

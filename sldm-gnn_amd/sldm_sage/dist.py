@@ -128,6 +128,19 @@ class HipBackend:
         return dense.sage_linear_bwd_weight(dh, agg, x)
 
     @staticmethod
+    def bwd_data_blocked_ok(dh, fi, cs):
+        """Whether :meth:`bwd_data_blocked` takes this dtype / shape."""
+        from . import dense
+        return dense.sage_linear_bwd_data_blocked_ok(dh, fi, cs)
+
+    @staticmethod
+    def bwd_data_blocked(dh, wcat_t, rowptr, fi, cs, dx_root):
+        """bwd_data on a row window with dAgg / deg written straight in the
+        all-to-all's send layout (flat [F_in / cs][rows][cs])."""
+        from . import dense
+        return dense.sage_linear_bwd_data_blocked(dh, wcat_t, rowptr, fi, cs, dx_root)
+
+    @staticmethod
     def cols_pack(rows, nblk, cs):
         """rows [n, nblk*cs] -> flat [nblk][n][cs] (layout.hip; torch for odd widths)."""
         from . import ops
@@ -782,9 +795,31 @@ class _FeatLayerFn(torch.autograd.Function):
         F = x.size(1)
         dh, dgamma, dbeta, dbl = be.post_bwd(dout.contiguous(), xhat, rstd, gamma, beta, slope,
                                              drop_p, seed, out, part.row_begin)
-        g, dx_r = be.bwd_data(dh, wl, wr, part.own_rowptr)
-        # dAgg/deg to column layout (RCCL stream) while the weight-grad GEMM runs
-        g_cols, works = _feat_rows_to_cols(part, g, group, be)
+        cs = part.col_sizes(F)
+        blocked = (part.world > 1 and all(c == cs[0] for c in cs)
+                   and getattr(be, "bwd_data_blocked_ok", None) is not None
+                   and be.bwd_data_blocked_ok(dh, F, cs[0]))
+        if blocked:
+            # the dX GEMM writes dAgg/deg chunk by chunk in the all-to-all's send
+            # layout (no packing copy); each chunk's exchange starts behind its GEMM
+            from .dense import weight_cat
+            wcat_t = weight_cat(wl, wr, dh.dtype).t().contiguous()
+            dx_r = dh.new_empty(part.num_rows, F)
+            g_cols = dh.new_empty(part.num_nodes, cs[part.rank])
+            works = []
+            for j in range(part.num_chunks):
+                a, b = part.own_chunk[j], part.own_chunk[j + 1]
+                send = (be.bwd_data_blocked(dh[a:b], wcat_t, part.own_rowptr[a: b + 1], F, cs[0],
+                                            dx_r[a:b]) if b > a else dh.new_empty(0))
+                recv = g_cols[part.chunk_start[j]: part.chunk_start[j + 1]]
+                w = _a2a(recv.view(-1), send, [n * cs[part.rank] for n in part.chunk_rows[j]],
+                         [(b - a) * c for c in cs], group)
+                if w is not None:                  # None: a staged (synchronous) exchange
+                    works.append((w, send))
+        else:
+            g, dx_r = be.bwd_data(dh, wl, wr, part.own_rowptr)
+            # dAgg/deg to column layout (RCCL stream) while the weight-grad GEMM runs
+            g_cols, works = _feat_rows_to_cols(part, g, group, be)
         dwl, dwr = be.bwd_weight(dh, agg, x)
         grads = (dwl, dbl, dwr, dgamma, dbeta)
         flat = torch.cat([t.reshape(-1).float() for t in grads])
@@ -1009,8 +1044,13 @@ def estimate_strategies(edge_index: torch.Tensor, num_nodes: int, world: int, ra
     # exchange overlaps the gathers / dense of other chunks, one chunk's worth
     # of it stays exposed (the halo path overlaps only halo-free rows: additive)
     feat_comm = 4 * (world - 1) * (r1 - r0) * fc * elem / link
+    # layout copies per layer (each reads and writes the rank's rows once): x
+    # and dAgg/deg packed for their exchanges, agg unpacked, dx unpacked + added,
+    # the dropout-free copy of the carried layer output; the bf16 F = 256 dX GEMM
+    # writes dAgg/deg in send layout itself (dense.sage_linear_bwd_data_blocked)
+    copies = 4 if (elem == 2 and feat == 256 and fc in (32, 64, 128)) else 5
     feat_comp = (2 * e * (fc * elem + 4) / _gather_rate(fc * elem) + dense_own
-                 + 5 * 2 * (r1 - r0) * row / _DENSE_BPS)         # + layout switches
+                 + copies * 2 * (r1 - r0) * row / _DENSE_BPS)
     feat_t = max(feat_comm, feat_comp) + feat_comm / _FEAT_CHUNKS
     rep_t = (2 * e * (row + 4) / _gather_rate(row)
              + _DENSE_BYTES_PER_ROW_FS * num_nodes * row / _DENSE_BPS)

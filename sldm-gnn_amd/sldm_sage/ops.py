@@ -326,6 +326,35 @@ def gemm_nt_rowscale(a: torch.Tensor, b: torch.Tensor, rowptr: torch.Tensor | No
     return (out, out2) if split else out
 
 
+def gemm_nt_rowscale_blocked_ok(a: torch.Tensor, nc: int, scale_cols: int, blk_cols: int) -> bool:
+    """Whether :func:`gemm_nt_rowscale_blocked` takes this dtype / shape."""
+    return (a.is_cuda and a.dtype in _DTYPE_CODE and a.stride(1) == 1 and a.stride(0) % 8 == 0
+            and bool(_lib.load().sldm_gemm_nt_rowscale_blocked_ok(
+                dtype_code(a), a.size(1), nc, scale_cols, blk_cols)))
+
+
+def gemm_nt_rowscale_blocked(a: torch.Tensor, b: torch.Tensor, rowptr: torch.Tensor | None,
+                             scale_cols: int, blk_cols: int, out2: torch.Tensor | None = None):
+    """C = a · b^T as :func:`gemm_nt_rowscale` (split=True), the scaled half
+    C[:, :scale_cols] / deg returned column-blocked: flat [scale_cols //
+    blk_cols][n][blk_cols] -- what :func:`cols_pack` makes of it, written by
+    the GEMM.  Returns (blocked, C[:, scale_cols:])."""
+    dev = _require_gpu(a, b, rowptr, out2)
+    assert a.stride(1) == 1 and b.is_contiguous() and a.dtype == b.dtype
+    n, k = a.shape
+    nc = b.size(0)
+    out = torch.empty(n * scale_cols, dtype=a.dtype, device=dev)
+    if out2 is None:
+        out2 = torch.empty(n, nc - scale_cols, dtype=a.dtype, device=dev)
+    assert out2.shape == (n, nc - scale_cols) and out2.stride(1) == 1 and out2.dtype == a.dtype
+    with _Timed("dense_bwd_data", (n * k + n * nc) * a.element_size()):
+        _lib.check(_lib.load().sldm_gemm_nt_rowscale_blocked(
+            dtype_code(a), a.data_ptr(), a.stride(0), k, b.data_ptr(), b.stride(0), n, nc,
+            _ptr(rowptr), scale_cols, out.data_ptr(), blk_cols, out2.data_ptr(), out2.stride(0),
+            _stream(dev)), "sldm_gemm_nt_rowscale_blocked")
+    return out, out2
+
+
 def gemm_tn(a: torch.Tensor, b0: torch.Tensor, b1: torch.Tensor | None, split: bool = False):
     """fp32 [a.size(1), b0.size(1)+b1.size(1)] = a^T · [b0 | b1] (sum over rows).
 

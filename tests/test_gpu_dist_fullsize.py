@@ -202,6 +202,15 @@ def test_small_powerlaw_halo_hub_split_two_ranks(dtype):
 
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_small_f256_feature_two_ranks(dtype):
+    """Feature slices at F = 256 on a small graph: in bf16 the backward's dX
+    GEMM writes dAgg / deg in the all-to-all's send layout (no packing copy);
+    same bitwise checks as the full-size case."""
+    _run(dict(kind="uniform", n=30_000, e=200_000, hd=[256, 256, 256], dtype=dtype,
+              strategy="feature"))
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
 def test_full_size_c5_halo_two_ranks(dtype):
     """BASELINE configs[4] (C5, power-law) on cost-balanced destination-row
     blocks with the halo exchange."""

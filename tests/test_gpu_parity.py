@@ -988,6 +988,43 @@ def test_fp32_stream_gemm_rowscale_vs_fp64_and_tile(m, k, nc, monkeypatch):
             assert torch.equal(run(True, rowptr, True), got)
 
 
+@pytest.mark.parametrize("m", [1, 63, 64, 1000, 70_001])
+@pytest.mark.parametrize("cs", [32, 64, 128])
+def test_gemm_nt_rowscale_blocked_equals_packed(m, cs):
+    """sldm_gemm_nt_rowscale_blocked: the dX GEMM writing dAgg / deg in the
+    column-blocked send layout of a feature-sliced partition equals, bit for
+    bit, the row-layout result put through the packing copy; the root-path half
+    is the plain call's; an unsupported shape is refused."""
+    from sldm_sage import build_graph, ops
+    from oracle.sage_ref import random_graph
+    fi = fo = 256
+    ei, _ = random_graph(m, 3 * m + 1, 1, seed=m + cs)
+    g = build_graph(ei.to(DEV), m)
+    gen = torch.Generator(device=DEV).manual_seed(m + cs)
+    dh = torch.randn(m, fo, generator=gen, device=DEV).bfloat16()
+    wt = (torch.randn(2 * fi, fo, generator=gen, device=DEV) / 16).bfloat16()
+    assert ops.gemm_nt_rowscale_blocked_ok(dh, 2 * fi, fi, cs)
+    assert not ops.gemm_nt_rowscale_blocked_ok(dh, 2 * fi, fi, 48)
+    assert not ops.gemm_nt_rowscale_blocked_ok(dh.float(), 2 * fi, fi, cs)
+    for rowptr in (g.rowptr, None):
+        lo, hi = ops.gemm_nt_rowscale(dh, wt, rowptr, fi, split=True)
+        blocked, hi_b = ops.gemm_nt_rowscale_blocked(dh, wt, rowptr, fi, cs)
+        torch.cuda.synchronize()
+        assert torch.equal(hi_b, hi)
+        assert torch.equal(blocked, ops.cols_pack(lo, fi // cs, cs))
+    # a row window of a larger problem (what the chunked backward passes)
+    if m >= 1000:
+        a, b = 130, 130 + 517
+        out2 = torch.empty(m, fi, dtype=dh.dtype, device=DEV)
+        blocked, _ = ops.gemm_nt_rowscale_blocked(dh[a:b], wt, g.rowptr[a: b + 1], fi, cs,
+                                                  out2=out2[a:b])
+        lo, hi = ops.gemm_nt_rowscale(dh, wt, g.rowptr, fi, split=True)
+        assert torch.equal(out2[a:b], hi[a:b])
+        assert torch.equal(blocked, ops.cols_pack(lo[a:b].contiguous(), fi // cs, cs))
+    with pytest.raises(Exception):
+        ops.gemm_nt_rowscale_blocked(dh, wt, g.rowptr, fi, 48)
+
+
 # ------------------------------------------------ overlapped (split) gather --
 @pytest.mark.parametrize("mean", [True, False])
 def test_overlapped_gather_split_is_bit_exact(mean):
