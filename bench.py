@@ -705,14 +705,22 @@ def main():
     step_roof = None
     if kern and not use_dist:
         flop = 3 * 2.0 * n * 2 * f * f * L        # fwd, dX, dW of [N,2F]x[2F,F] per layer
-        t_star = step_bytes / (HBM_PEAK_GBS * 1e9) + flop / (MFMA_PEAK_TFLOPS[dtype] * 1e12)
-        t_star_copy = step_bytes / (HBM_COPY_GBS * 1e9) + flop / (MFMA_PEAK_TFLOPS[dtype] * 1e12)
+        # fp32 GEMMs run as six bf16 MFMA products per fp32 product (the default;
+        # SLDM_FP32_GEMM=exact selects the fp32 MFMA): price what is issued
+        split = dtype == torch.float32 and not os.environ.get("SLDM_FP32_GEMM", "").startswith("e")
+        t_mfma = (6 * flop / (MFMA_PEAK_TFLOPS[torch.bfloat16] * 1e12) if split
+                  else flop / (MFMA_PEAK_TFLOPS[dtype] * 1e12))
+        t_star = step_bytes / (HBM_PEAK_GBS * 1e9) + t_mfma
+        t_star_copy = step_bytes / (HBM_COPY_GBS * 1e9) + t_mfma
         step_roof = dict(bytes_per_step=int(step_bytes), flop_per_step=flop,
                          t_star_ms=round(t_star * 1e3, 3),
                          frac=round(t_star / (elapsed / args.steps), 4),
                          frac_vs_measured_copy=round(t_star_copy / (elapsed / args.steps), 4),
-                         note="T* = bytes/8 TB/s + FLOP/dense MFMA peak; "
-                              "frac_vs_measured_copy prices bytes at the 6.29 TB/s copy ceiling")
+                         note="T* = bytes/8 TB/s + FLOP/dense MFMA peak"
+                              + (" (fp32 as six bf16 MFMA products: 6 x FLOP at the bf16 peak)"
+                                 if split else "")
+                              + "; frac_vs_measured_copy prices bytes at the 6.29 TB/s copy "
+                                "ceiling")
     kernels = {k: dict(avg_ms=round(v["avg_ms"], 4), launches=v["launches"],
                        gbs=round(v["avg_bytes"] / (v["avg_ms"] * 1e-3) / 1e9, 1))
                for k, v in kern.items()}
