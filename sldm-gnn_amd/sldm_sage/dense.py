@@ -58,6 +58,41 @@ def sage_linear_bwd_data_blocked(dh: torch.Tensor, wcat_t: torch.Tensor, rowptr:
     return blocked
 
 
+class SageLinearFn(torch.autograd.Function):
+    """out = agg · W_l^T + b_l + x · W_r^T, the dense half of a stand-alone
+    SAGEConv (PyG 2.7.0 ``SAGEConv.forward``: ``lin_l(out) + lin_r(x_r)``), on
+    the library's MFMA GEMMs: one NT GEMM over [agg | x] forward, the dX GEMM
+    and the row-streaming dW GEMM backward (no rocBLAS / hipBLASLt)."""
+
+    @staticmethod
+    def forward(ctx, agg, x, wl, bl, wr):
+        wcat = weight_cat(wl, wr, x.dtype)                           # [F_out, 2 F_in]
+        a = torch.cat([agg, x], dim=1)
+        out = ops.gemm_nt_rowscale(a, wcat, None, 0)
+        if bl is not None:
+            out += bl.to(out.dtype)
+        ctx.save_for_backward(agg, x, wcat)
+        ctx.meta = (wl.dtype, wr.dtype, None if bl is None else bl.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        agg, x, wcat = ctx.saved_tensors
+        wl_dt, wr_dt, bl_dt = ctx.meta
+        fi = x.size(1)
+        dout = dout.contiguous()
+        dagg = dx = dwl = dbl = dwr = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            d = ops.gemm_nt_rowscale(dout, wcat.t().contiguous(), None, 0)   # [N, 2 F_in]
+            dagg, dx = d[:, :fi], d[:, fi:]
+        if ctx.needs_input_grad[2] or ctx.needs_input_grad[4]:
+            dwl, dwr = ops.gemm_tn(dout, agg, x, split=True)                 # fp32
+            dwl, dwr = dwl.to(wl_dt), dwr.to(wr_dt)
+        if bl_dt is not None and ctx.needs_input_grad[3]:
+            dbl = dout.float().sum(0).to(bl_dt)
+        return dagg, dx, dwl, dbl, dwr
+
+
 def sage_linear_bwd_weight(dh: torch.Tensor, agg: torch.Tensor, x: torch.Tensor):
     """(dW_l, dW_r) = (dh^T · agg, dh^T · x), fp32, one launch + its reduce
     writing both (no slicing copies)."""

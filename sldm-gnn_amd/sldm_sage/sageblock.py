@@ -149,6 +149,13 @@ class SageConv(nn.Module):
     def forward(self, x: torch.Tensor, edge_index) -> torch.Tensor:
         """Stand-alone conv (no post stack): lin_l(mean_j x_j) + lin_r(x)."""
         agg = sage_aggregate(x, edge_index)
+        if x.device.type == "cuda":
+            # the library's MFMA GEMMs, in x's storage dtype (fp32 or bf16) with fp32
+            # accumulation, like the SageBlock's fused layers
+            from .dense import SageLinearFn
+            xs = x if x.dtype in (torch.float32, torch.bfloat16) else x.float()
+            return SageLinearFn.apply(agg.to(xs.dtype), xs, self.lin_l.weight, self.lin_l.bias,
+                                      self.lin_r.weight)
         out = nn.functional.linear(agg.to(self.lin_l.weight.dtype), self.lin_l.weight,
                                    self.lin_l.bias)
         return out + nn.functional.linear(x.to(self.lin_r.weight.dtype), self.lin_r.weight)

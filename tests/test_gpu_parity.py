@@ -639,6 +639,43 @@ def test_graph_cache_static_and_invalidate():
     assert len(graph_cache) == 0
 
 
+@pytest.mark.parametrize("n,e,fi,fo", [(500, 3000, 16, 24), (3000, 20000, 256, 256),
+                                       (1000, 0, 32, 8)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_standalone_sageconv_vs_oracle(n, e, fi, fo, dtype):
+    """SageConv used on its own (PyG ``SAGEConv.forward``: lin_l(mean_j x_j) +
+    lin_r(x), no post stack) runs the library's gather and MFMA GEMMs; forward
+    and every gradient against the oracle's RefSAGEConv (fp32 on the CPU)."""
+    from sldm_sage import SageConv
+    from oracle.sage_ref import RefSAGEConv, random_graph
+    ei, x = random_graph(n, max(e, 1), fi, seed=n + fo)
+    if e == 0:
+        ei = ei[:, :0]
+    torch.manual_seed(fi)
+    ref = RefSAGEConv(fi, fo)
+    conv = SageConv(fi, fo)
+    conv.load_state_dict(ref.state_dict())                 # same keys, strict
+    conv = conv.to(DEV)
+    gout = torch.randn(n, fo, generator=torch.Generator().manual_seed(5))
+    xs = x.to(dtype)
+    xr = xs.float().clone().requires_grad_(True)
+    ref(xr, ei).backward(gout.to(dtype).float())
+    xd = xs.detach().clone().to(DEV).requires_grad_(True)
+    out = conv(xd, ei.to(DEV))
+    assert out.dtype == dtype
+    out.backward(gout.to(dtype).to(DEV))
+    torch.cuda.synchronize()
+    tol = dict(atol=1e-4, rtol=1e-4) if dtype == torch.float32 else dict(atol=3e-2, rtol=2e-2)
+    with torch.no_grad():
+        torch.testing.assert_close(out.float().cpu(), ref(xs.float(), ei), **tol)
+    torch.testing.assert_close(xd.grad.float().cpu(), xr.grad, **tol)
+    for (k, pg), (_, pr) in zip(conv.named_parameters(), ref.named_parameters()):
+        s = max(1.0, pr.grad.abs().max().item())
+        torch.testing.assert_close(pg.grad.cpu() / s, pr.grad / s,
+                                   atol=1e-4 if dtype == torch.float32 else 1e-2, rtol=1e-3,
+                                   msg=lambda m, k=k: f"{k}: {m}")
+
+
 # ------------------------------------------------------------- MFMA GEMMs --
 GEMM_SHAPES = [  # (M, F_in, F_out)
     (1000, 16, 16), (777, 128, 128), (300, 256, 256), (513, 96, 96), (200, 10, 8),
