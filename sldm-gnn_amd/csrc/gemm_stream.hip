@@ -40,7 +40,6 @@ typedef short s8v __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_vptr;
 
-constexpr int kThreads = 512;   // ROWSCALE kernels: 8 waves, one workgroup per CU
 // LN forward launch shape: waves per workgroup (8: one 512-thread workgroup
 // per CU; 4: two 256-thread workgroups per CU, whose k-step barriers are
 // independent, so one workgroup's epilogue VALU can overlap the other's loads
