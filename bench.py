@@ -373,7 +373,42 @@ def bench_map(args, dev):
 
     t = _time_steps(step, args.warmup, args.steps)
     E = ei.size(1)
+
+    # The same step as one captured HIP graph (static lane graph, fixed shapes):
+    # the operators allocate from the graph's pool and sync nothing, so forward +
+    # backward replay as a single launch.  Without dropout: a captured dropout
+    # seed would repeat its mask every replay (the inference / eval case, or a
+    # block built with dropout=None).
+    blk_g = SageBlock([16, 32, 32], dropout=None, negative_slope=0.1).to(dev).train()
+    sx = x.detach().clone().requires_grad_(True)
+    sg = torch.ones(S, 32, device=dev)
+    side_stream = torch.cuda.Stream()
+    side_stream.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side_stream):
+        for _ in range(3):
+            blk_g.zero_grad(set_to_none=True)
+            sx.grad = None
+            blk_g(sx, ei).backward(sg)
+    torch.cuda.current_stream().wait_stream(side_stream)
+    torch.cuda.synchronize()
+    blk_g.zero_grad(set_to_none=True)
+    sx.grad = None
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        blk_g(sx, ei).backward(sg)
+
+    def eager_nodrop():
+        blk_g.zero_grad(set_to_none=True)
+        xr = x.detach().requires_grad_(True)
+        blk_g(xr, ei).backward(sg)
+
+    t_graph = _time_steps(graph.replay, args.warmup, args.steps)
+    t_eager = _time_steps(eager_nodrop, args.warmup, args.steps)
     return {"metric": "edges/sec SageBlock fwd+bwd (lane map)", "value": round(E * 2 / t, 1),
+            "hip_graph": {"ms_per_step": round(t_graph * 1e3, 3),
+                          "eager_ms_per_step_same_block": round(t_eager * 1e3, 3),
+                          "what": "forward + backward of the block with dropout=None captured "
+                                  "once with torch.cuda.graph and replayed"},
             "unit": "edges/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp32",
