@@ -8,9 +8,9 @@ planner's max-reduce, the partition setup, DistSageBlock's exchanges, the
 locality-variant second run, the max-over-ranks timing and rank 0's JSON line
 all run as at N > 1.  The times are not a measurement (the line says so).
 
-Round 1 saw one 8-rank run abort in a rank (HIP runtime, during a torch
-reduction) and one 4-rank run hang in gloo.  What those runs had in common
-was gloo's own CUDA path: device tensors handed to gloo collectives (its
+An earlier form of this flow once aborted in a rank (HIP runtime, during a
+torch reduction, 8 ranks) and once hung in gloo (4 ranks).  What those runs
+had in common was gloo's own CUDA path: device tensors handed to gloo collectives (its
 internal streams and pinned staging, racing the kernels on the current
 stream and the caching allocator), plus a halo-exchange skip decided per
 rank.  sldm_sage.dist now stages every gloo collective on device tensors
