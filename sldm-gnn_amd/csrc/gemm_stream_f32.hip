@@ -54,8 +54,9 @@ constexpr int IMG = 256 * 64;     // bytes of one bf16 image of a 32-deep slice 
 constexpr int WSTAGE = 3 * IMG;   // hi | mid | lo
 
 enum { SF_LN = 0, SF_ROWSCALE = 1 };
-// Diagnostic builds only (tools/ab_build.sh; results wrong): 1 = no MFMAs,
-// 6 = no split arithmetic (raw bits as fragments).
+// Diagnostic builds only (tools/ab_build.sh; results wrong, timing only):
+// 1 = no MFMAs, 6 = no split arithmetic (raw bits as fragments), 8 = no
+// activation reloads, 9 = no weight reloads, 10 = no output stores.
 #ifndef SLDM_SF_EXP
 #define SLDM_SF_EXP 0
 #endif
@@ -270,8 +271,12 @@ __global__ __launch_bounds__(kThreads) void gemm_stream_x6_kernel(SfArgs p) {
           // registers reloaded with pieces 2, 3, which go half a step later
           const int r = (t >> 1) & 1, pc = (t >= 8 ? 2 : 0) + r;
           store_w1((ks + 1) & 1, pc, wraw[r], ln);
+#if SLDM_SF_EXP != 9      // diagnostic 9: no weight reloads (timing only)
           if (t < 8) load_w1((ks + 1) % KSTEPS, pc + 2, wraw[r], ln);
           else load_w1((ks + 2) % KSTEPS, pc - 2, wraw[r], ln);
+#else
+          asm volatile("" : "+v"(wraw[r]));
+#endif
         }
         if (t == NTT - 1) {
           // after the step's last MFMAs have issued: their operands' registers
@@ -280,13 +285,22 @@ __global__ __launch_bounds__(kThreads) void gemm_stream_x6_kernel(SfArgs p) {
           __builtin_amdgcn_sched_barrier(0);
           split_a(araw[0], af[0]);
           split_a(araw[1], af[1]);
+#if SLDM_SF_EXP != 8      // diagnostic 8: no activation reloads (timing only)
           if (ks + 2 < KSTEPS) load_a(tile, ks + 2, araw, ln);
           else load_a(next, ks + 2 - KSTEPS, araw, ln);
+#else
+          asm volatile("" : "+v"(araw[0][0]), "+v"(araw[0][1]), "+v"(araw[1][0]), "+v"(araw[1][1]));
+#endif
         }
         __builtin_amdgcn_sched_barrier(0);
       }
     }
 
+#if SLDM_SF_EXP == 10    // diagnostic 10: no output stores (timing only)
+#define SF_STORE(ptr, v) do { if (p.eps < 0.f) *reinterpret_cast<f4v*>(ptr) = (v); } while (0)
+#else
+#define SF_STORE(ptr, v) (*reinterpret_cast<f4v*>(ptr) = (v))
+#endif
     const int q = lane_id() >> 4, r16 = lane_id() & 15;
     // ---- epilogue: acc[m][t][r] = C[row 16m + r16][col 16t + 4q + r] ----
     if constexpr (MODE == SF_LN) {
@@ -328,7 +342,7 @@ __global__ __launch_bounds__(kThreads) void gemm_stream_x6_kernel(SfArgs p) {
         for (int t = 0; t < NTT; ++t) {
           const int c = 16 * t + cq;
           const f4v xh = acc[m][t] * rs;
-          if (xrow) *reinterpret_cast<f4v*>(xrow + 16 * t) = xh;
+          if (xrow) SF_STORE(xrow + 16 * t, xh);
           const f4v gg = *reinterpret_cast<const f4v*>(prm + 256 + c);
           const f4v be = *reinterpret_cast<const f4v*>(prm + 512 + c);
           bool keep[4] = {true, true, true, true};
@@ -343,7 +357,7 @@ __global__ __launch_bounds__(kThreads) void gemm_stream_x6_kernel(SfArgs p) {
             const float a = y > 0.f ? y : y * p.slope;
             o[r] = keep[r] ? a * p.drop_scale : 0.f;
           }
-          *reinterpret_cast<f4v*>(orow + 16 * t) = o;
+          SF_STORE(orow + 16 * t, o);
         }
       }
     } else {
@@ -368,10 +382,11 @@ __global__ __launch_bounds__(kThreads) void gemm_stream_x6_kernel(SfArgs p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) o[r] = o[r] / cnt;
           }
-          *reinterpret_cast<f4v*>(orow + 16 * t) = o;
+          SF_STORE(orow + 16 * t, o);
         }
       }
     }
+#undef SF_STORE
 
     if (!has_next) break;
     tile = next;
