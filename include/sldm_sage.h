@@ -18,7 +18,11 @@
  *   - return value: SLDM_OK or an error code; sldm_last_error() then returns a
  *     thread-local message.  Launch failures are reported from hipGetLastError.
  *   - thread safety: safe from any host thread; the only global state is the
- *     per-device address of sldm_gather_rows_split_static's scratch array.
+ *     per-device address of sldm_gather_rows_split_static's scratch array
+ *     (sldm_set_dropout_seed_source is per host thread);
+ *   - HIP graph capture: every entry point only launches kernels on `stream`
+ *     (no memset or copy nodes, no synchronisation), so a caller may record
+ *     them into a graph; see sldm_set_dropout_seed_source for dropout.
  */
 #ifndef SLDM_SAGE_H
 #define SLDM_SAGE_H
@@ -30,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SLDM_ABI_VERSION 8   /* 8: + sldm_gemm_nt_rowscale_blocked(_ok) */
+#define SLDM_ABI_VERSION 9   /* 9: + sldm_set_dropout_seed_source; 8: + sldm_gemm_nt_rowscale_blocked(_ok) */
 
 enum sldm_dtype { SLDM_F32 = 0, SLDM_BF16 = 1 };
 enum sldm_status { SLDM_OK = 0, SLDM_ERR_ARG = 1, SLDM_ERR_HIP = 2 };
@@ -144,6 +148,18 @@ int sldm_scale_rows_by_inv_deg(int dtype, void* d, int64_t ld, const int32_t* ro
  * are saved for the backward when non-NULL.  The dropout key of row i is
  * (seed, i + row_offset): a rank holding rows [r0, r1) of a partitioned graph
  * passes row_offset = r0 and draws the single-device mask. */
+/* Dropout seeds of launches recorded into a HIP graph (nn.Dropout inside
+ * sageblock.py:13 draws a new mask per call; a kernel argument is frozen at
+ * capture).  While `device_word` is non-NULL, every launch this host thread
+ * makes through an entry point that takes a `seed` keys its mask with
+ * seed + *device_word (mod 2^64), the word read on the device when the kernel
+ * runs: change the word between replays (a captured increment, or a copy from
+ * the host) and each replay drops a different mask, the backward launches of
+ * the same replay regenerating the forward's.  The word must stay allocated as
+ * long as a graph holding such launches can run.  NULL (the initial state)
+ * restores plain host seeds.  Per host thread; affects no launch already made. */
+void sldm_set_dropout_seed_source(const uint64_t* device_word);
+
 int sldm_post_fwd(int h_dtype, const void* h, int64_t ldh, int64_t num_rows, int64_t feat,
                   const float* bias, const float* gamma, const float* beta, float eps,
                   float negative_slope, float drop_p, uint64_t seed, int64_t row_offset,

@@ -302,7 +302,7 @@ extern "C" int sldm_batch_graphs(int64_t num_graphs, const int64_t* const* edge_
   SLDM_REQUIRE(out_ld >= e_total && (e_total == 0 || (out_edge_index && col)),
                "sldm_batch_graphs: output edge_index / col missing or too short");
   hipStream_t stream = sldm::as_stream(stream_);
-  SLDM_HIP_CHECK(hipMemsetAsync(bad_index_flag, 0, sizeof(int32_t), stream));
+  if (const int rc = sldm::zero_words(bad_index_flag, 1, stream); rc != SLDM_OK) return rc;
   const size_t lds_cnt = (size_t)(2 * max_n + kThreads) * sizeof(int32_t);
   const size_t lds_ids = lds_cnt + (size_t)2 * max_e * sizeof(int32_t);
   const size_t lds_stg = lds_cnt + (size_t)4 * max_e * sizeof(int32_t);

@@ -12,6 +12,9 @@ namespace sldm {
 // Thread-local last-error message (sldm_last_error()).
 void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 void clear_error();
+// Zero `words` 32-bit words at `ptr` with a kernel on `stream` (not a memset
+// node: every launch of the library may be recorded into a HIP graph).
+int zero_words(void* ptr, size_t words, void* stream);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -198,6 +201,22 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x *= 0x846ca68bu;
   x ^= x >> 16;
   return x;
+}
+// Dropout seed of one launch: the caller's 64-bit value plus, when the calling
+// thread has set a device seed source (sldm_set_dropout_seed_source), the word
+// that pointer names, read by the kernel when it runs -- a launch recorded
+// into a HIP graph then draws a new mask on every replay whose seed word the
+// graph (or the host) has changed.  Host code converts a plain value at the
+// first internal call; kernels take the pair and call effective_seed once.
+const uint64_t* seed_source();
+struct Seed {
+  uint64_t value;
+  const uint64_t* dev;
+  Seed() = default;
+  Seed(uint64_t v) : value(v), dev(seed_source()) {}
+};
+__device__ __forceinline__ uint64_t effective_seed(const Seed& s) {
+  return s.dev ? s.value + *s.dev : s.value;
 }
 __device__ __forceinline__ uint32_t dropout_row_key(uint64_t seed, uint64_t row) {
   return hash32((uint32_t)seed ^ hash32((uint32_t)(seed >> 32) ^ hash32((uint32_t)row) ^

@@ -144,10 +144,9 @@ extern "C" int sldm_csr_build(const void* edge_index, int index_is_int64, int64_
   hipStream_t stream = sldm::as_stream(stream_);
 
   if (E == 0) {
-    SLDM_HIP_CHECK(hipMemsetAsync(rowptr, 0, sizeof(int32_t) * (size_t)(N + 1), stream));
-    if (t_rowptr)
-      SLDM_HIP_CHECK(hipMemsetAsync(t_rowptr, 0, sizeof(int32_t) * (size_t)(N + 1), stream));
-    return SLDM_OK;
+    int rc = sldm::zero_words(rowptr, (size_t)(N + 1), stream);
+    if (rc == SLDM_OK && t_rowptr) rc = sldm::zero_words(t_rowptr, (size_t)(N + 1), stream);
+    return rc;
   }
   SLDM_REQUIRE(edge_index != nullptr && col != nullptr,
                "sldm_csr_build: edge_index / col must not be NULL");

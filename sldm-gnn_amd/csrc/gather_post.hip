@@ -38,7 +38,7 @@ __global__ __launch_bounds__(kBlock) void gather_post_bwd_kernel(
     const int32_t* __restrict__ t_col, const int32_t* __restrict__ order,
     const T* __restrict__ addend, int64_t lda, int64_t nrows, int feat, int lpr_log2,
     const T* __restrict__ xhat, const float* __restrict__ rstd, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float slope, float drop_p, float drop_scale, uint64_t seed,
+    const float* __restrict__ beta, float slope, float drop_p, float drop_scale, sldm::Seed seed,
     int64_t row_off, T* __restrict__ dh, float* __restrict__ partials) {
   // Contraction off, as in post_bwd_kernel: the same explicit fmas, every
   // other product and sum rounded on its own -> bit-identical dh.
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(kBlock) void gather_post_bwd_kernel(
     // ---- post backward of the layer below on that row (post.hip's math)
     const float* gbr = gb;
     asm volatile("" : "+v"(gbr));   // per-row LDS reads, not loop-invariant registers
-    const uint32_t rkey = sldm::dropout_row_key(seed, (uint64_t)(row + row_off));
+    const uint32_t rkey = sldm::dropout_row_key(sldm::effective_seed(seed), (uint64_t)(row + row_off));
     float gx[NCH][V], dy[NCH][V];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll

@@ -81,7 +81,7 @@ struct NtArgs {
   // EPI_LN
   T* xhat; float* rstd;
   const float* bias; const float* gamma; const float* beta;
-  float eps, slope, drop_p, drop_scale; uint64_t seed; int64_t row_off;
+  float eps, slope, drop_p, drop_scale; sldm::Seed seed; int64_t row_off;
   // EPI_ROWSCALE (out2: optional destination of the columns >= scale_cols)
   const int32_t* rowptr; int scale_cols;
   T* out2; int64_t ldo2;
@@ -184,7 +184,7 @@ __device__ __forceinline__ void nt_row_epilogue(const NtArgs<T>& p, const float*
       const float rstd = 1.0f / sqrtf(sldm::group_sum(sq, lpr) * inv_n + p.eps);
       if (p.rstd && (lane & (lpr - 1)) == 0) p.rstd[row] = rstd;
       if (!lane_on) continue;
-      const uint32_t rkey = sldm::dropout_row_key(p.seed, (uint64_t)(row + p.row_off));
+      const uint32_t rkey = sldm::dropout_row_key(sldm::effective_seed(p.seed), (uint64_t)(row + p.row_off));
       float xh[4], z[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1330,13 +1330,9 @@ int gemm_tn_impl(int dtype, const void* a, int64_t lda, int64_t mo, const void* 
   hipStream_t stream = sldm::as_stream(stream_);
   const int64_t nn = n0 + n1;
   if (num_rows == 0) {
-    if (out1) {
-      SLDM_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * (size_t)(mo * n0), stream));
-      SLDM_HIP_CHECK(hipMemsetAsync(out1, 0, sizeof(float) * (size_t)(mo * n1), stream));
-    } else {
-      SLDM_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * (size_t)(mo * nn), stream));
-    }
-    return SLDM_OK;
+    if (!out1) return sldm::zero_words(out, (size_t)(mo * nn), stream);
+    const int rc = sldm::zero_words(out, (size_t)(mo * n0), stream);
+    return rc != SLDM_OK ? rc : sldm::zero_words(out1, (size_t)(mo * n1), stream);
   }
   const size_t need = sldm_gemm_tn_workspace_bytes(num_rows, mo, nn);
   SLDM_REQUIRE(workspace && ws_bytes >= need, "sldm_gemm_tn: workspace too small (%zu < %zu)",

@@ -47,7 +47,7 @@ struct BigArgs {
   uint16_t* out; int64_t ldo;
   uint16_t* xhat; float* rstd;
   const float* bias; const float* gamma; const float* beta;
-  float eps, slope, drop_p, drop_scale; uint64_t seed; int64_t row_off;
+  float eps, slope, drop_p, drop_scale; sldm::Seed seed; int64_t row_off;
   const int32_t* rowptr; int scale_cols;
   uint16_t* out2; int64_t ldo2;               // optional home of columns >= scale_cols
 };
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_big_kernel(BigArgs p) {
       const int64_t row = m0 + 64 * wm + 16 * m + r16;
       if (row >= p.M) continue;
       if (p.rstd && q == 0 && wn == 0) p.rstd[row] = rstdv[m];
-      const uint32_t rkey = sldm::dropout_row_key(p.seed, (uint64_t)(row + p.row_off));
+      const uint32_t rkey = sldm::dropout_row_key(sldm::effective_seed(p.seed), (uint64_t)(row + p.row_off));
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int c = cbase + 16 * t;

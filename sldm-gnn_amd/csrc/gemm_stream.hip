@@ -80,7 +80,7 @@ struct StreamArgs {
   uint16_t* out; int64_t ldo;
   uint16_t* xhat; float* rstd;
   const float* bias; const float* gamma; const float* beta;
-  float eps, slope, drop_p, drop_scale; uint64_t seed; int64_t row_off;
+  float eps, slope, drop_p, drop_scale; sldm::Seed seed; int64_t row_off;
   const int32_t* rowptr; int scale_cols;
   uint16_t* out2; int64_t ldo2;               // ROWSCALE: optional home of columns >= scale_cols
 };
@@ -349,7 +349,7 @@ __global__ __launch_bounds__(NW * 64, 2) void gemm_stream_kernel(StreamArgs p) {
         const float rs = 1.0f / sqrtf(v2 * inv_n + p.eps);
 #pragma unroll
         for (int t = 0; t < NTT; ++t) acc[m][t] *= rs;
-        const uint32_t rkey = sldm::dropout_row_key(p.seed, (uint64_t)(row + p.row_off));
+        const uint32_t rkey = sldm::dropout_row_key(sldm::effective_seed(p.seed), (uint64_t)(row + p.row_off));
 #endif
         if (p.rstd && q == 0) p.rstd[row] = rs;
 

@@ -69,7 +69,7 @@ struct SfArgs {
   float* out; int64_t ldo;
   float* xhat; float* rstd;
   const float* bias; const float* gamma; const float* beta;
-  float eps, slope, drop_p, drop_scale; uint64_t seed; int64_t row_off;
+  float eps, slope, drop_p, drop_scale; sldm::Seed seed; int64_t row_off;
   const int32_t* rowptr; int scale_cols;
   float* out2; int64_t ldo2;           // ROWSCALE: optional home of columns >= scale_cols
 };
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(kThreads) void gemm_stream_x6_kernel(SfArgs p) {
         v2 = sldm::row4_sum(v2);
         const float rs = 1.0f / sqrtf(v2 * inv_n + p.eps);
         if (p.rstd && q == 0) p.rstd[row] = rs;
-        const uint32_t rkey = sldm::dropout_row_key(p.seed, (uint64_t)(row + p.row_off));
+        const uint32_t rkey = sldm::dropout_row_key(sldm::effective_seed(p.seed), (uint64_t)(row + p.row_off));
         float* xrow = p.xhat ? p.xhat + row * p.ldo + cq : nullptr;
         float* orow = p.out + row * p.ldo + cq;
 #pragma unroll

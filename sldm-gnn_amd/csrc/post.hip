@@ -20,7 +20,7 @@ __global__ __launch_bounds__(kBlock) void post_fwd_kernel(
     const TH* __restrict__ h, int64_t ldh, int64_t nrows, int feat, int lpr_log2,
     const float* __restrict__ bias, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float slope, float drop_p, float drop_scale,
-    uint64_t seed, int64_t row_off, TO* __restrict__ out, TO* __restrict__ xhat_out, float* __restrict__ rstd_out) {
+    sldm::Seed seed, int64_t row_off, TO* __restrict__ out, TO* __restrict__ xhat_out, float* __restrict__ rstd_out) {
   const int lpr = 1 << lpr_log2;
   const int lane_in_row = threadIdx.x & (lpr - 1);
   const int64_t row = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> lpr_log2;
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(kBlock) void post_fwd_kernel(
   const float rstd = 1.0f / sqrtf(var + eps);
   if (!live) return;
   if (rstd_out && lane_in_row == 0) rstd_out[row] = rstd;
-  const uint32_t rkey = sldm::dropout_row_key(seed, (uint64_t)(row + row_off));
+  const uint32_t rkey = sldm::dropout_row_key(sldm::effective_seed(seed), (uint64_t)(row + row_off));
   const uint32_t dthr = sldm::dropout_threshold(drop_p);
 
 #pragma unroll
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
     const T* __restrict__ dout, const T* __restrict__ xhat, const T* __restrict__ zout,
     const float* __restrict__ rstd,
     int64_t nrows, int feat, int lpr_log2, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float slope, float drop_p, float drop_scale, uint64_t seed, int64_t row_off,
+    const float* __restrict__ beta, float slope, float drop_p, float drop_scale, sldm::Seed seed, int64_t row_off,
     TD* __restrict__ dh, float* __restrict__ partials) {
   // Contraction off: every product rounds on its own and the fmas are the
   // explicit ones, so gather_post.hip's fused copy of this math gives the
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(kBlock) void post_bwd_kernel(
     for (int u = 0; u < RB; ++u) {
       const int64_t r = rr[u];
       const float rs = rsv[u];
-      const uint32_t rkey = sldm::dropout_row_key(seed, (uint64_t)(r + row_off));
+      const uint32_t rkey = sldm::dropout_row_key(sldm::effective_seed(seed), (uint64_t)(r + row_off));
       float gx[NCH][V], dy[NCH][V];
       float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll

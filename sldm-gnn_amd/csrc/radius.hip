@@ -167,8 +167,7 @@ extern "C" int sldm_radius_edges(const float* pos, int64_t pos_sv, int64_t pos_s
   SLDM_REQUIRE(num_edges, "sldm_radius_edges: NULL num_edges");
   hipStream_t stream = sldm::as_stream(stream_);
   if (num_vehicles == 0) {
-    SLDM_HIP_CHECK(hipMemsetAsync(num_edges, 0, sizeof(int32_t), stream));
-    return SLDM_OK;
+    return sldm::zero_words(num_edges, 1, stream);
   }
   SLDM_REQUIRE(pos && presence && edge_index && edge_attr,
                "sldm_radius_edges: NULL argument");

@@ -15,7 +15,7 @@ import torch  # noqa: F401  (must be imported before the HIP library)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SLDM_SAGE_LIB", os.path.join(_HERE, "libsldm_sage.so"))
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 F32, BF16 = 0, 1
 
 _c_i64 = ctypes.c_int64
@@ -26,6 +26,7 @@ _vp = ctypes.c_void_p
 _SIGNATURES = {
     "sldm_abi_version": (ctypes.c_int, []),
     "sldm_last_error": (ctypes.c_char_p, []),
+    "sldm_set_dropout_seed_source": (None, [ctypes.c_void_p]),
     "sldm_csr_workspace_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
     "sldm_csr_build": (ctypes.c_int, [_vp, ctypes.c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp,
                                       _vp, _vp, ctypes.c_size_t, _vp]),

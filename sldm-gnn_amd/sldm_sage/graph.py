@@ -51,6 +51,7 @@ class SageGraph:
     hub: HubPlan | None = None            # high-degree split of rowptr rows (skewed graphs)
     t_hub: HubPlan | None = None          # same for t_rowptr
     _packed: tuple | None = None
+    bad: torch.Tensor | None = None       # device range flag of a build that could not read it
 
     @property
     def device(self) -> torch.device:
@@ -82,12 +83,23 @@ class SageGraph:
     def in_degree(self) -> torch.Tensor:
         return self.rowptr[1:] - self.rowptr[:-1]
 
+    def check(self) -> None:
+        """Raise IndexError if the build found a node id out of range: for
+        graphs built under HIP graph capture, whose build leaves the flag on
+        the device (call after a replay has finished; one host sync)."""
+        if self.bad is not None and int(self.bad) != 0:
+            raise IndexError(f"edge_index holds a node id outside [0, {self.num_nodes})")
+
 
 # Skew handling (power-law graphs).  Graphs below HUB_MIN_EDGES are
 # launch-bound (per-batch vehicle graphs: ~10^4 edges) and skip it -- and its
 # host sync -- entirely.  SLDM_SKEW: "split" (default: hub rows split into
 # chunks) or "none".
 HUB_MIN_EDGES = int(os.environ.get("SLDM_HUB_MIN_EDGES", str(1 << 20)))
+# Largest edge count whose CSR build may be recorded into a HIP graph: above
+# it the radix sort inside sldm_csr_build clears its histograms with memset
+# nodes (rocPRIM's one-sweep path), which a captured graph must not hold.
+CAPTURE_MAX_EDGES = 1 << 20
 HUB_CHUNK = 256          # edges per hub chunk (one row group sums one chunk)
 
 
@@ -118,6 +130,18 @@ def build_graph(edge_index: torch.Tensor, num_nodes: int, transpose: bool = True
         from . import cpu
         rowptr, col, t_rowptr, t_col = cpu.csr_build(edge_index, num_nodes, transpose)
         return SageGraph(num_nodes, E, rowptr, col, t_rowptr, t_col)
+    if torch.cuda.is_current_stream_capturing():
+        # recorded into a HIP graph (a per-batch edge_index buffer refilled
+        # between replays): no host read is possible, so the range flag stays
+        # on the device (SageGraph.check; the kernels clamp a bad id to node 0)
+        # and rows are never split -- per-batch graphs are far below that size
+        if E > CAPTURE_MAX_EDGES:
+            raise RuntimeError(
+                f"a graph of {E} edges cannot be built under HIP graph capture (limit "
+                f"{CAPTURE_MAX_EDGES}): build it before the capture (sldm_sage.build_graph) "
+                "and pass the SageGraph")
+        rowptr, col, t_rowptr, t_col, bad = ops.csr_build(edge_index, num_nodes, transpose)
+        return SageGraph(num_nodes, E, rowptr, col, t_rowptr, t_col, bad=bad)
     rowptr, col, t_rowptr, t_col, bad = ops.csr_build(edge_index, num_nodes, transpose)
     g = SageGraph(num_nodes, E, rowptr, col, t_rowptr, t_col)
     mode = _skew_mode()
@@ -179,10 +203,13 @@ class _GraphCache:
             self._entries.pop(key, None)
 
     def get(self, edge_index: torch.Tensor, num_nodes: int, transpose: bool) -> SageGraph:
-        if edge_index.is_inference():
+        if edge_index.is_inference() or (edge_index.device.type == "cuda"
+                                         and torch.cuda.is_current_stream_capturing()):
             # Inference tensors carry no version counter: an in-place edit
             # would go unseen, so they are never cached (rcv.py builds a new
-            # graph per pack anyway).
+            # graph per pack anyway).  A build recorded into a HIP graph has
+            # not run yet: its arrays hold nothing until a replay, so no
+            # eager call may find it in the cache.
             return build_graph(edge_index, num_nodes, transpose=transpose)
         key = id(edge_index)
         ver = edge_index._version
@@ -207,7 +234,8 @@ class _GraphCache:
     def put(self, edge_index: torch.Tensor, num_nodes: int, graph: SageGraph) -> None:
         """Register a CSR built elsewhere (e.g. at collate time) for this
         edge_index tensor, so the next SageBlock call skips the GPU build."""
-        if edge_index.is_inference() or graph.device != edge_index.device:
+        if edge_index.is_inference() or graph.device != edge_index.device or (
+                edge_index.device.type == "cuda" and torch.cuda.is_current_stream_capturing()):
             return
         key = id(edge_index)
         try:

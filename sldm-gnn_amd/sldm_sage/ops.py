@@ -117,6 +117,73 @@ class _Timed:
         return False
 
 
+# -------------------------------------------------- dropout under capture --
+class dropout_seed_source:
+    """While active, every dropout-keyed launch this thread makes through the
+    library adds the int64 word of ``word`` (a 1-element device tensor), read
+    on the device when the kernel runs, to its seed
+    (``sldm_set_dropout_seed_source``): launches recorded into a HIP graph
+    then draw a new mask on every replay that finds a new value there.
+    ``None`` is a no-op."""
+
+    __slots__ = ("word",)
+
+    def __init__(self, word: torch.Tensor | None):
+        if word is not None and (word.dtype != torch.int64 or word.numel() != 1
+                                 or word.device.type != "cuda"):
+            raise TypeError("dropout_seed_source: a 1-element int64 device tensor")
+        self.word = word
+
+    def __enter__(self):
+        if self.word is not None:
+            _lib.load().sldm_set_dropout_seed_source(self.word.data_ptr())
+        return self
+
+    def __exit__(self, *exc):
+        if self.word is not None:
+            _lib.load().sldm_set_dropout_seed_source(None)
+        return False
+
+
+_SEED_COUNTERS: dict[int, torch.Tensor] = {}
+_SEED_STEP = 0x2545F4914F6CDD1D & (2**62 - 1)      # odd: the counter visits every value
+
+
+def capture_seed_counter(device: torch.device, create: bool = True) -> torch.Tensor | None:
+    """The device's dropout counter for HIP graph capture: one int64 word in
+    [0, 2^62), advanced by a fixed odd step by every captured SageBlock call
+    that drops (so each replay, and each call inside a replay, keys its masks
+    anew).  Created -- outside any capture -- from the state of the device's
+    default generator (torch.manual_seed governs it); ``create=False`` returns
+    None when it does not exist yet."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    t = _SEED_COUNTERS.get(idx)
+    if t is None and create:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError(
+                "the dropout counter of HIP graph capture must exist before the capture "
+                "begins: run one training call of the block eagerly first (the warm-up "
+                "torch.cuda.graph asks for anyway) or call "
+                "sldm_sage.ops.capture_seed_counter(device)")
+        # keyed by the generator's seed and offset, without advancing it: an
+        # eager call's masks do not depend on whether the counter exists yet
+        from .sageblock import _splitmix64
+        gen = torch.cuda.default_generators[idx]
+        v = _splitmix64(gen.initial_seed() ^ _splitmix64(gen.get_offset() ^ 0x5EED)) & (2**62 - 1)
+        t = torch.tensor([v], dtype=torch.int64, device=torch.device("cuda", idx))
+        _SEED_COUNTERS[idx] = t
+    return t
+
+
+def next_capture_seed(device: torch.device) -> torch.Tensor:
+    """Advance the device's counter and return a copy of its new value, both
+    as launches on the current stream (recorded when it is capturing): the
+    seed word of one SageBlock call."""
+    c = capture_seed_counter(device)
+    c.add_(_SEED_STEP).bitwise_and_(2**62 - 1)
+    return c.clone()
+
+
 # ------------------------------------------------------------------ graph --
 def csr_build(edge_index: torch.Tensor, num_nodes: int, transpose: bool = True):
     """edge_index [2,E] (int64/int32, on the GPU) -> (rowptr, col, t_rowptr, t_col, bad).

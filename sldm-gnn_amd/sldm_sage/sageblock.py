@@ -104,16 +104,18 @@ class _SageStackFn(torch.autograd.Function):
     row order)."""
 
     @staticmethod
-    def forward(ctx, x, graph: SageGraph, cfgs, *params):
+    def forward(ctx, x, graph: SageGraph, cfgs, seed_word, *params):
         sldm = torch_ops.load()
         gl, gm = graph.packed()
         slopes = [c[0] for c in cfgs]
         drops = [c[1] for c in cfgs]
         seeds = [c[2] for c in cfgs]
         eps = [c[3] for c in cfgs]
-        res = sldm.sage_stack_fwd(x, gl, gm, params, slopes, drops, seeds, eps, True)
+        with ops.dropout_seed_source(seed_word):
+            res = sldm.sage_stack_fwd(x, gl, gm, params, slopes, drops, seeds, eps, True)
         ctx.save_for_backward(*res[1:], *params)
         ctx.graph, ctx.cfg, ctx.nl = graph, (slopes, drops, seeds), len(cfgs)
+        ctx.seed_word = seed_word
         return res[0]
 
     @staticmethod
@@ -124,9 +126,10 @@ class _SageStackFn(torch.autograd.Function):
         slopes, drops, seeds = ctx.cfg
         gl, gm = ctx.graph.packed()
         need_dx = ctx.needs_input_grad[0]
-        grads = torch.ops.sldm.sage_stack_bwd(dout, saved, gl, gm, params, slopes, drops, seeds,
-                                              need_dx, True)
-        return (grads[0] if need_dx else None, None, None, *grads[1:])
+        with ops.dropout_seed_source(ctx.seed_word):
+            grads = torch.ops.sldm.sage_stack_bwd(dout, saved, gl, gm, params, slopes, drops,
+                                                  seeds, need_dx, True)
+        return (grads[0] if need_dx else None, None, None, None, *grads[1:])
 
 
 class SageConv(nn.Module):
@@ -206,20 +209,34 @@ class SageBlock(nn.Module):
         if x.dtype not in (torch.float32, torch.bfloat16):
             x = x.float()
         x = x.contiguous()
+        drops = any(_drop_p(post[2]) > 0 for post in self.posts)
+        # Recorded into a HIP graph, a host seed would freeze one mask into every
+        # replay: the call's seed is then a device word (the device's capture
+        # counter, advanced by a recorded launch) that the kernels add to the
+        # layer index at run time.
+        seed_word = None
+        if drops and torch.cuda.is_current_stream_capturing():
+            if not (grad and FUSE_BOUNDARIES):
+                raise RuntimeError("SageBlock: dropout under HIP graph capture runs on the fused "
+                                   "training stack only (grad enabled, SLDM_FUSE_BOUNDARIES on)")
+            seed_word = ops.next_capture_seed(x.device)
+        elif drops and grad:
+            ops.capture_seed_counter(x.device)      # exists before any capture begins
         layers = []
         for conv, post in zip(self.convs, self.posts):
             ln, act, drop = post[0], post[1], post[2]
             if not isinstance(ln, nn.LayerNorm) or ln.weight is None:
                 raise TypeError("SageBlock post[0] must be an affine LayerNorm")
             p = _drop_p(drop)
+            seed = 0 if p <= 0 else (len(layers) if seed_word is not None
+                                     else _new_seed(x.device))
             layers.append(((conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, ln.weight,
-                            ln.bias), (_act_slope(act), p, _new_seed(x.device) if p > 0 else 0,
-                                       float(ln.eps))))
+                            ln.bias), (_act_slope(act), p, seed, float(ln.eps))))
         if grad and FUSE_BOUNDARIES:
             # training: one autograd node for the stack (fused layer boundaries)
             cfgs = tuple(c for _, c in layers)
             params = [t for w, _ in layers for t in w]
-            return _SageStackFn.apply(x, graph, cfgs, *params)
+            return _SageStackFn.apply(x, graph, cfgs, seed_word, *params)
         for (wl, bl, wr, gamma, beta), (slope, p, seed, eps) in layers:
             x = sage_layer(x, graph, wl, bl, wr, gamma, beta, slope, p, seed, eps)
         return x
