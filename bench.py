@@ -326,6 +326,52 @@ def bench_vehicle(args, dev):
         tb = torch_ops_gpu_baseline(blk, b.edge_index, b.x, gout, warmup=2, steps=10)
         if tb:
             t_ref.append(tb)
+    # The same training step (dropout on) as ONE captured HIP graph at padded
+    # shapes: every batch is written into static buffers (feature rows past the
+    # batch zero, the unused tail of edge_index filled with the padding edge
+    # (N, N) that the CSR build ignores), and a replay runs the CSR build of that
+    # edge_index, the forward and the backward; the dropout seed is a device
+    # word advanced inside the graph.
+    n_pad, e_pad = max(nodes), max(edges)
+    padded = []
+    for pool in pools[:4]:
+        b = collate([dict(p) for p in pool])
+        n, e = b.x.size(0), b.edge_index.size(1)
+        xp = torch.zeros(n_pad, hd[0], device=dev)
+        xp[:n] = b.x
+        eip = torch.full((2, e_pad), n_pad, dtype=torch.int64, device=dev)
+        eip[:, :e] = b.edge_index
+        gp = torch.zeros(n_pad, hd[-1], device=dev)
+        gp[:n] = 1.0
+        padded.append((xp, eip, gp))
+    sx = padded[0][0].clone().requires_grad_(True)
+    sei, sg = padded[0][1].clone(), padded[0][2].clone()
+    side_stream = torch.cuda.Stream()
+    side_stream.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side_stream):
+        for _ in range(3):
+            blk.zero_grad(set_to_none=True)
+            sx.grad = None
+            blk(sx, sei.clone()).backward(sg)
+    torch.cuda.current_stream().wait_stream(side_stream)
+    torch.cuda.synchronize()
+    blk.zero_grad(set_to_none=True)
+    sx.grad = None
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        blk(sx, sei).backward(sg)
+    git = [0]
+
+    def graph_step():
+        xp, eip, gp = padded[git[0] % len(padded)]
+        git[0] += 1
+        with torch.no_grad():
+            sx.copy_(xp)
+            sei.copy_(eip)
+            sg.copy_(gp)
+        graph.replay()
+
+    t_graph = _time_steps(graph_step, args.warmup, args.steps)
     e_avg, n_avg = sum(edges) / len(edges), sum(nodes) / len(nodes)
     return {"metric": "edges/sec SageBlock fwd+bwd (vehicle batches)", "value": round(
         e_avg * (len(hd) - 1) / t, 1), "unit": "edges/s", "n_gpus": 1, "steps": args.steps,
@@ -337,6 +383,13 @@ def bench_vehicle(args, dev):
                    "edges_per_batch": round(e_avg), "dropout": 0.25, "negative_slope": 0.1},
         "graphs_per_s": round(PACKS_PER_BATCH / t, 1),
         "sageblock_only_ms": round(statistics.median(t_own) * 1e3, 3),
+        "hip_graph": {"ms_per_step": round(t_graph * 1e3, 3),
+                      "padded_nodes": n_pad, "padded_edges": e_pad,
+                      "what": "three device copies of a padded batch into static buffers + one "
+                              "replay of the captured training step (CSR build of the batch's "
+                              "edge_index, forward, backward; dropout 0.25 keyed by a device "
+                              "word the graph advances); compare with sageblock_only_ms, whose "
+                              "CSR comes from collate"},
         "torch_ops_gpu_baseline": ({"ms_per_step": round(statistics.median(t_ref) * 1e3, 3),
                                     "speedup_vs_sageblock_only": round(
                                         statistics.median(t_ref) / statistics.median(t_own), 2),
@@ -376,10 +429,9 @@ def bench_map(args, dev):
 
     # The same step as one captured HIP graph (static lane graph, fixed shapes):
     # the operators allocate from the graph's pool and sync nothing, so forward +
-    # backward replay as a single launch.  Without dropout: a captured dropout
-    # seed would repeat its mask every replay (the inference / eval case, or a
-    # block built with dropout=None).
-    blk_g = SageBlock([16, 32, 32], dropout=None, negative_slope=0.1).to(dev).train()
+    # backward replay as a single launch; the dropout seed is a device word the
+    # graph advances, so every replay drops a new mask.
+    blk_g = blk
     sx = x.detach().clone().requires_grad_(True)
     sg = torch.ones(S, 32, device=dev)
     side_stream = torch.cuda.Stream()
@@ -407,8 +459,9 @@ def bench_map(args, dev):
     return {"metric": "edges/sec SageBlock fwd+bwd (lane map)", "value": round(E * 2 / t, 1),
             "hip_graph": {"ms_per_step": round(t_graph * 1e3, 3),
                           "eager_ms_per_step_same_block": round(t_eager * 1e3, 3),
-                          "what": "forward + backward of the block with dropout=None captured "
-                                  "once with torch.cuda.graph and replayed"},
+                          "what": "forward + backward of the same block (dropout 0.25, a new "
+                                  "mask per replay) captured once with torch.cuda.graph and "
+                                  "replayed"},
             "unit": "edges/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp32",

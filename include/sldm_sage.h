@@ -54,7 +54,13 @@ const char* sldm_last_error(void);
  * order in which PyG's CPU scatter_add_ accumulates.
  * edge_index is [2,E] (row 0 = source, row 1 = target), int64 if
  * index_is_int64 else int32.  Any id outside [0,N) sets *bad_index_flag
- * (device int32, caller-zeroed) to 1; outputs are then unspecified.
+ * (device int32, caller-zeroed) to 1; outputs are then unspecified -- except
+ * that an edge (N, N) is PADDING and is ignored (no counterpart in the
+ * reference, where it would raise): a fixed-shape edge_index buffer, as a
+ * captured HIP graph needs, fills its unused tail with it; rowptr[N] is then
+ * the number of real edges and col / t_col hold them in front.
+ * More than 2^20 edges: the sort inside records memset nodes, so such a build
+ * must not be captured into a HIP graph (build it before the capture).
  * Requires N < 2^31 and E < 2^31.  t_rowptr/t_col may be NULL (forward only). */
 size_t sldm_csr_workspace_bytes(int64_t num_edges, int64_t num_nodes);
 int sldm_csr_build(const void* edge_index, int index_is_int64, int64_t num_edges,

@@ -8,8 +8,10 @@
 // scatter_add_ accumulates (oracle/csr_ref.c states the same contract in C).
 //
 // Integer work, HBM-bound: one pass to narrow/validate ids to int32, an LSD
-// radix sort (rocPRIM, stable) on ceil(log2 N) key bits, and one pass that
-// turns the sorted keys into row pointers without atomics.
+// radix sort (rocPRIM, stable) on ceil(log2 (N+1)) key bits, and one pass that
+// turns the sorted keys into row pointers without atomics.  An edge (N, N) is
+// padding (fixed-shape edge_index buffers of captured graphs): its key N sorts
+// behind row N-1, past rowptr[N], where no kernel reads.
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "common.hpp"
@@ -26,7 +28,8 @@ __global__ __launch_bounds__(kBlock) void narrow_validate_kernel(
   if (e >= E) return;
   int64_t s = (int64_t)ei[e];
   int64_t d = (int64_t)ei[E + e];
-  bool ok = (s >= 0) & (s < N) & (d >= 0) & (d < N);
+  // (N, N) is a padding edge: it keeps key N and sorts behind every row
+  bool ok = ((s >= 0) & (s < N) & (d >= 0) & (d < N)) | ((s == N) & (d == N));
   if (!ok) {
     atomicOr(bad, 1);
     s = 0;
@@ -69,7 +72,7 @@ size_t sort_temp_bytes(int64_t E, int64_t N) {
   if (E == 0) return 0;
   (void)rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                   (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)E, 0u,
-                                  key_bits(N), (hipStream_t)0);
+                                  key_bits(N + 1), (hipStream_t)0);
   return bytes;
 }
 
@@ -162,7 +165,7 @@ extern "C" int sldm_csr_build(const void* edge_index, int index_is_int64, int64_
   uint32_t* keys_out = reinterpret_cast<uint32_t*>(ws + 2 * arr);
   void* temp = ws + 3 * arr;
   size_t temp_bytes = sort_temp_bytes(E, N);
-  const unsigned bits = key_bits(N);
+  const unsigned bits = key_bits(N + 1);    // keys in [0, N]: N marks padding edges
 
   const unsigned grid_e = (unsigned)((E + kBlock - 1) / kBlock);
   if (index_is_int64)

@@ -49,19 +49,24 @@ extern "C" {
 
 // CSR by destination (rowptr, col = sources) and by source (t_rowptr,
 // t_col = destinations), each row in original edge order (stable counting
-// sort).  Returns 1 if an id is outside [0, N), else 0.
+// sort).  Returns 1 if an id is outside [0, N), else 0.  An edge (N, N) is
+// padding and is skipped, as in the GPU build.
 int sldm_cpu_csr_build(const int64_t* ei, int64_t E, int64_t N, int32_t* rowptr, int32_t* col,
                        int32_t* t_rowptr, int32_t* t_col) {
   const int64_t* src = ei;
   const int64_t* dst = ei + E;
-  for (int64_t e = 0; e < E; ++e)
+  for (int64_t e = 0; e < E; ++e) {
+    if (src[e] == N && dst[e] == N) continue;
     if (src[e] < 0 || src[e] >= N || dst[e] < 0 || dst[e] >= N) return 1;
+  }
   auto build = [&](const int64_t* key, const int64_t* val, int32_t* ptr, int32_t* out) {
     std::fill(ptr, ptr + N + 1, 0);
-    for (int64_t e = 0; e < E; ++e) ptr[key[e] + 1]++;
+    for (int64_t e = 0; e < E; ++e)
+      if (key[e] < N) ptr[key[e] + 1]++;
     for (int64_t i = 0; i < N; ++i) ptr[i + 1] += ptr[i];
     std::vector<int32_t> pos(ptr, ptr + N);
-    for (int64_t e = 0; e < E; ++e) out[pos[key[e]]++] = (int32_t)val[e];
+    for (int64_t e = 0; e < E; ++e)
+      if (key[e] < N) out[pos[key[e]]++] = (int32_t)val[e];
   };
   build(dst, src, rowptr, col);
   if (t_rowptr) build(src, dst, t_rowptr, t_col);

@@ -54,3 +54,22 @@ def test_cpu_sageblock_contract():
         blk.eval()
         out = blk(x, ei)
         assert out.shape == (20, 8)
+
+
+def test_cpu_csr_build_ignores_padding_edges():
+    """Edges (N, N) are padding on the CPU path as on the GPU: the block's
+    output on a padded edge_index equals the output on the real edges."""
+    from sldm_sage import SageBlock, cpu
+    from oracle.sage_ref import random_graph
+    n, e = 300, 2000
+    ei, x = random_graph(n, e, 16, seed=9)
+    padded = torch.cat([ei[:, :1000], torch.full((2, 57), n, dtype=torch.int64), ei[:, 1000:]], 1)
+    a, b = cpu.csr_build(ei, n), cpu.csr_build(padded, n)
+    for u, v, k in zip(a, b, (n + 1, e, n + 1, e)):
+        assert torch.equal(u[:k], v[:k])
+    torch.manual_seed(0)
+    blk = SageBlock([16, 32], None, 0.1).eval()
+    with torch.no_grad():
+        assert torch.equal(blk(x, ei), blk(x, padded))
+    with pytest.raises(IndexError):
+        cpu.csr_build(torch.tensor([[n], [0]]), n)

@@ -107,11 +107,11 @@ def test_sageblock_training_step_replays_in_a_hip_graph(dtype, hd):
 
 def _padded_batch(n_real, e_real, n_pad, e_pad, feat, seed, dtype):
     """A batch's graph padded to the captured shapes: random edges among the
-    first n_real nodes, the unused tail of edge_index filled with self-loops
-    on the last (padding) node, feature rows past n_real zero."""
+    first n_real nodes, the unused tail of edge_index filled with the padding
+    edge (N, N) that the CSR build ignores, feature rows past n_real zero."""
     g = torch.Generator().manual_seed(seed)
     ei = torch.randint(0, n_real, (2, e_real), generator=g)
-    pad = torch.full((2, e_pad - e_real), n_pad - 1, dtype=torch.int64)
+    pad = torch.full((2, e_pad - e_real), n_pad, dtype=torch.int64)
     x = torch.zeros(n_pad, feat)
     x[:n_real] = torch.randn(n_real, feat, generator=g)
     return torch.cat([ei, pad], 1).to(DEV), x.to(DEV).to(dtype)

@@ -39,6 +39,26 @@ def test_csr_build_bit_exact(n, e, idx_dtype):
     assert np.array_equal(g.t_col.cpu().numpy(), tcol)
 
 
+@pytest.mark.parametrize("n,e,pad", [(1000, 5000, 700), (4096, 30000, 1), (1, 0, 3)])
+def test_csr_build_ignores_padding_edges(n, e, pad):
+    """Edges (N, N) -- the filler of a fixed-shape edge_index buffer -- leave
+    the CSR of the real edges unchanged, wherever they sit in the buffer
+    (N = 4096: the padding key needs one more sort bit than the node ids)."""
+    from sldm_sage import build_graph
+    ei, _ = _graph(n, e, 1, seed=n + e)
+    padded = torch.cat([ei[:, : e // 2], torch.full((2, pad), n, dtype=torch.int64),
+                        ei[:, e // 2:]], 1)
+    g = build_graph(padded.to(DEV), n)
+    rp, col, trp, tcol = ref_csr(ei, n)
+    assert np.array_equal(g.rowptr.cpu().numpy(), rp)
+    assert np.array_equal(g.col.cpu().numpy()[:e], col)
+    assert np.array_equal(g.t_rowptr.cpu().numpy(), trp)
+    assert np.array_equal(g.t_col.cpu().numpy()[:e], tcol)
+    half = torch.tensor([[0], [n]], device=DEV)          # only one end at N: a bad id
+    with pytest.raises(IndexError):
+        build_graph(half, n)
+
+
 def test_csr_power_law_hub():
     """One node with in-degree 10k plus duplicates and self loops."""
     from sldm_sage import build_graph
