@@ -773,7 +773,7 @@ def main():
         traffic = None
         pmc = os.path.join(ROOT, "profiles", PMC_SUMMARY)
         if (args.config == "c4" and args.graph == "uniform" and world == 1
-                and os.path.exists(pmc)):
+                and dtype == torch.bfloat16 and os.path.exists(pmc)):
             # HBM bytes per launch of this kernel at this workload, from the
             # committed rocprofv3 PMC passes (2*FETCH_SIZE + WRITE_SIZE).
             with open(pmc) as fh:
