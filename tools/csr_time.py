@@ -1,3 +1,5 @@
+"""Time ops.csr_build (with and without the transpose CSR) at per-batch and
+large graph sizes on the GPU: python tools/csr_time.py"""
 import sys, torch
 sys.path.insert(0, "sldm-gnn_amd")
 from sldm_sage import ops
