@@ -361,10 +361,12 @@ PostBwd gather_post_bwd(const Tensor& g, const GraphView& gr, const Tensor& adde
 }
 
 // [dAgg / deg | dx_root] = dh [W_l | W_r] as two contiguous [N, F_in] tensors
-std::pair<Tensor, Tensor> bwd_data(const Tensor& dh, const Tensor& wcat, const Tensor& rowptr) {
+std::pair<Tensor, Tensor> bwd_data(const Tensor& dh, const Tensor& wl, const Tensor& wr,
+                                   const Tensor& rowptr) {
   const int64_t n = dh.size(0), k = dh.size(1);
-  const int64_t fi = wcat.size(1) / 2;
-  Tensor wt = wcat.t().contiguous();                       // [2 F_in, F_out]
+  const int64_t fi = wl.size(1);
+  // [W_l | W_r]^T = [W_l^T ; W_r^T], [2 F_in, F_out], built by one copy kernel
+  Tensor wt = at::cat({wl.t(), wr.t()}, 0).to(dh.scalar_type()).contiguous();
   void* st = stream_of(dh);
   Timed timed("dense_bwd_data", (double)(n * k + n * 2 * fi) * dh.element_size(), st);
   if (fi % 4 == 0) {
@@ -517,8 +519,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> op_sage_layer_bwd(
   if (need_dx) {
     TORCH_CHECK(g.has_t, "SageGraph was built without its transpose; rebuild with transpose=True "
                          "for backward");
-    Tensor wcat = weight_cat(wl, wr, x.scalar_type());
-    auto [gd, dxr] = bwd_data(pb.dh, wcat, g.rowptr);
+    auto [gd, dxr] = bwd_data(pb.dh, wl, wr, g.rowptr);
     dx = gather(gd, g.t_rowptr, g.t_col, nullptr, x.size(0), false, &dxr, Tensor(), g.t_hub,
                 "gather_bwd");
   }
@@ -597,8 +598,7 @@ std::vector<Tensor> op_sage_stack_bwd(const Tensor& dout, at::TensorList saved,
     grads[1 + 5 * i + 3] = as_dtype(pb.dgamma, gamma);
     grads[1 + 5 * i + 4] = as_dtype(pb.dbeta, beta);
     if (i == 0 && !need_dx) break;
-    Tensor wcat = weight_cat(wl, wr, h.scalar_type());
-    auto [gd, dxr] = bwd_data(pb.dh, wcat, g.rowptr);
+    auto [gd, dxr] = bwd_data(pb.dh, wl, wr, g.rowptr);
     if (i == 0) {
       grads[0] = gather(gd, g.t_rowptr, g.t_col, nullptr, h.size(0), false, &dxr, Tensor(),
                         g.t_hub, "gather_bwd");
