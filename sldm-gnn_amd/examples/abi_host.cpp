@@ -4,7 +4,12 @@
 // on the GPU, runs the mean aggregation (the reference's index_select +
 // scatter-mean, sageblock.py:18) and its transpose-gather backward, and checks
 // both bit for bit against a host restatement of the reference's order (fp32
-// sums in edge order, one bf16 rounding).  Exit status 0 on success.
+// sums in edge order, one bf16 rounding).  Then the same three launches are
+// recorded into a HIP graph (up to 2^20 edges) and replayed on new edge lists
+// whose tail is padding -- edges (N, N), which the build ignores -- and a
+// LayerNorm + dropout launch is recorded with a device seed word: replays
+// with different words drop different masks, and a replay equals the eager
+// launch whose seed is value + word.  Exit status 0 on success.
 //   usage: abi_host [num_nodes num_edges feat]
 #include <hip/hip_runtime.h>
 
@@ -129,9 +134,109 @@ int main(int argc, char** argv) {
   std::printf("abi_host: N=%d E=%lld F=%d csr %s, mean gather %s, transpose gather %s\n", n,
               (long long)E, F, (rp == hrp && col == hcol && trp == htrp && tcol == htcol) ? "equal" : "DIFFERS",
               out == hout ? "bit-exact" : "DIFFERS", dx == hdx ? "bit-exact" : "DIFFERS");
+  bool cap_ok = true, drop_ok = true;
+  if (E > 0 && E <= ((int64_t)1 << 20)) {
+    // ---- CSR build + both gathers as one captured graph, replayed on new edges ----
+    hipGraph_t graph;
+    hipGraphExec_t exec;
+    HIP_OK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    SLDM_CALL(sldm_csr_build(d_ei, 1, E, n, d_rp, d_col, d_trp, d_tcol, d_bad, d_ws, ws, st));
+    SLDM_CALL(sldm_gather_rows(SLDM_BF16, d_x, F, d_rp, d_col, nullptr, n, F, 1, nullptr, 0,
+                               SLDM_BF16, d_out, F, st));
+    SLDM_CALL(sldm_gather_rows(SLDM_BF16, d_x, F, d_trp, d_tcol, nullptr, n, F, 0, d_add, F,
+                               SLDM_BF16, d_dx, F, st));
+    HIP_OK(hipStreamEndCapture(st, &graph));
+    HIP_OK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    for (int rep = 0; rep < 3 && cap_ok; ++rep) {
+      const int64_t real = rep == 1 ? E / 3 : E - E / 8;       // the rest of the buffer is padding
+      std::vector<int64_t> padded(2 * E, (int64_t)n), re(2 * real);
+      for (int64_t e = 0; e < real; ++e) {
+        re[e] = padded[e] = (int64_t)(lcg(seed) % (uint64_t)n);
+        re[real + e] = padded[E + e] = (int64_t)(lcg(seed) % (uint64_t)n);
+      }
+      HIP_OK(hipMemcpy(d_ei, padded.data(), sizeof(int64_t) * 2 * E, hipMemcpyHostToDevice));
+      // the program's own eager work between replays
+      SLDM_CALL(sldm_gather_rows(SLDM_BF16, d_add, F, d_rp, d_col, nullptr, n, F, 1, nullptr, 0,
+                                 SLDM_BF16, d_out, F, st));
+      HIP_OK(hipStreamSynchronize(st));
+      HIP_OK(hipGraphLaunch(exec, st));
+      HIP_OK(hipStreamSynchronize(st));
+      HIP_OK(hipMemcpy(&bad, d_bad, sizeof(int32_t), hipMemcpyDeviceToHost));
+      HIP_OK(hipMemcpy(rp.data(), d_rp, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
+      HIP_OK(hipMemcpy(col.data(), d_col, sizeof(int32_t) * E, hipMemcpyDeviceToHost));
+      HIP_OK(hipMemcpy(trp.data(), d_trp, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
+      HIP_OK(hipMemcpy(tcol.data(), d_tcol, sizeof(int32_t) * E, hipMemcpyDeviceToHost));
+      HIP_OK(hipMemcpy(out.data(), d_out, sizeof(uint16_t) * out.size(), hipMemcpyDeviceToHost));
+      HIP_OK(hipMemcpy(dx.data(), d_dx, sizeof(uint16_t) * dx.size(), hipMemcpyDeviceToHost));
+      host_csr(re, real, n, true, hrp, hcol);
+      host_csr(re, real, n, false, htrp, htcol);
+      host_gather(hrp, hcol, x, nullptr, F, true, hout);
+      host_gather(htrp, htcol, x, &add, F, false, hdx);
+      col.resize(real);
+      tcol.resize(real);
+      cap_ok = bad == 0 && rp == hrp && col == hcol && trp == htrp && tcol == htcol &&
+               out == hout && dx == hdx;
+      col.resize(E);
+      tcol.resize(E);
+    }
+    std::printf("abi_host: captured graph, 3 replays on new padded edge lists %s\n",
+                cap_ok ? "bit-exact" : "DIFFERS");
+    (void)hipGraphExecDestroy(exec);
+    (void)hipGraphDestroy(graph);
+
+    // ---- dropout under capture: the mask is keyed by seed + *word ----
+    const size_t nf = (size_t)n * F;
+    std::vector<float> h(nf), gam(F, 1.25f), bet(F, 0.1f), oa(nf), ob(nf), oc(nf);
+    for (auto& v : h) v = ((float)(lcg(seed) % 20001) - 10000.f) / 4096.f;
+    float *d_h, *d_gam, *d_bet, *d_o;
+    uint64_t* d_word;
+    HIP_OK(hipMalloc(&d_h, sizeof(float) * nf));
+    HIP_OK(hipMalloc(&d_o, sizeof(float) * nf));
+    HIP_OK(hipMalloc(&d_gam, sizeof(float) * F));
+    HIP_OK(hipMalloc(&d_bet, sizeof(float) * F));
+    HIP_OK(hipMalloc(&d_word, sizeof(uint64_t)));
+    HIP_OK(hipMemcpy(d_h, h.data(), sizeof(float) * nf, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_gam, gam.data(), sizeof(float) * F, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_bet, bet.data(), sizeof(float) * F, hipMemcpyHostToDevice));
+    auto post = [&](uint64_t sd) {
+      return sldm_post_fwd(SLDM_F32, d_h, F, n, F, nullptr, d_gam, d_bet, 1e-5f, 0.1f, 0.25f, sd, 0,
+                           SLDM_F32, d_o, nullptr, nullptr, st);
+    };
+    HIP_OK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    sldm_set_dropout_seed_source(d_word);
+    SLDM_CALL(post(7));
+    sldm_set_dropout_seed_source(nullptr);
+    HIP_OK(hipStreamEndCapture(st, &graph));
+    HIP_OK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    const uint64_t words[2] = {100, 200};
+    std::vector<float>* outs[2] = {&oa, &ob};
+    for (int rep = 0; rep < 2; ++rep) {
+      HIP_OK(hipMemcpy(d_word, &words[rep], sizeof(uint64_t), hipMemcpyHostToDevice));
+      HIP_OK(hipGraphLaunch(exec, st));
+      HIP_OK(hipStreamSynchronize(st));
+      HIP_OK(hipMemcpy(outs[rep]->data(), d_o, sizeof(float) * nf, hipMemcpyDeviceToHost));
+    }
+    SLDM_CALL(post(7 + 200));                      // eager, host seed only
+    HIP_OK(hipStreamSynchronize(st));
+    HIP_OK(hipMemcpy(oc.data(), d_o, sizeof(float) * nf, hipMemcpyDeviceToHost));
+    size_t zeros = 0;
+    for (float v : ob) zeros += v == 0.f;
+    drop_ok = std::memcmp(ob.data(), oc.data(), sizeof(float) * nf) == 0 &&
+              std::memcmp(oa.data(), ob.data(), sizeof(float) * nf) != 0 &&
+              zeros > nf / 5 && zeros < nf * 3 / 10;
+    std::printf("abi_host: dropout seed word: replay == eager(seed + word) %s, masks of two "
+                "words %s, dropped fraction %.3f\n",
+                std::memcmp(ob.data(), oc.data(), sizeof(float) * nf) == 0 ? "bit-exact" : "DIFFERS",
+                std::memcmp(oa.data(), ob.data(), sizeof(float) * nf) != 0 ? "differ" : "DIFFERS NOT",
+                (double)zeros / (double)nf);
+    (void)hipGraphExecDestroy(exec);
+    (void)hipGraphDestroy(graph);
+    for (void* ptr : {(void*)d_h, (void*)d_o, (void*)d_gam, (void*)d_bet, (void*)d_word})
+      (void)hipFree(ptr);
+  }
   for (void* ptr : {(void*)d_ei, (void*)d_x, (void*)d_add, (void*)d_out, (void*)d_dx,
                     (void*)d_rp, (void*)d_trp, (void*)d_col, (void*)d_tcol, (void*)d_bad, d_ws})
     (void)hipFree(ptr);
   (void)hipStreamDestroy(st);
-  return ok ? 0 : 1;
+  return ok && cap_ok && drop_ok ? 0 : 1;
 }

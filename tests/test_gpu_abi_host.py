@@ -1,8 +1,11 @@
 """The C ABI driven by a non-Python host (sldm-gnn_amd/examples/abi_host.cpp,
 built by __graft_entry__.build()): CSR build, mean gather and transpose
 gather from plain C++ + the HIP runtime, checked bit for bit against the
-program's own host restatement of the reference's order.  Run as a child
-process (never exec'd from this GPU-initialised process)."""
+program's own host restatement of the reference's order; then (up to 2^20
+edges) the same launches recorded with hipStreamBeginCapture and replayed on
+new edge lists padded with (N, N) edges, and a LayerNorm + dropout launch
+recorded with a device seed word (sldm_set_dropout_seed_source).  Run as a
+child process (never exec'd from this GPU-initialised process)."""
 import os
 import subprocess
 
