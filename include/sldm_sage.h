@@ -22,7 +22,10 @@
  *     (sldm_set_dropout_seed_source is per host thread);
  *   - HIP graph capture: every entry point only launches kernels on `stream`
  *     (no memset or copy nodes, no synchronisation), so a caller may record
- *     them into a graph; see sldm_set_dropout_seed_source for dropout.
+ *     them into a graph -- with one exception: the radix sorts inside
+ *     sldm_csr_build and sldm_degree_order switch, above 2^20 items, to a path
+ *     that clears its histograms with memset nodes (build such graphs before
+ *     the capture).  See sldm_set_dropout_seed_source for dropout.
  */
 #ifndef SLDM_SAGE_H
 #define SLDM_SAGE_H
