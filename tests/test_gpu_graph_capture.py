@@ -149,8 +149,11 @@ def test_per_batch_graph_forward_replays_in_a_hip_graph():
         assert torch.equal(static_out, eager)
 
 
-@pytest.mark.parametrize("dtype,hd", [(torch.float32, [64, 64, 64]),
-                                      (torch.bfloat16, [256, 256, 256])])
+@pytest.mark.parametrize("dtype,hd", [(torch.float32, [64, 64, 64]),        # tile kernels
+                                      (torch.bfloat16, [256, 256, 256]),     # bf16 stream kernels
+                                      (torch.float32, [256, 256]),           # fp32 stream kernels
+                                      (torch.bfloat16, [128, 128, 128]),     # big-tile kernel
+                                      (torch.float32, [16, 32, 32])])        # the lane-map block
 def test_per_batch_training_step_with_dropout_replays_in_a_hip_graph(dtype, hd, monkeypatch):
     """The reference's training step on a pack (utils.py:218-227: train mode,
     dropout on, a new edge_index per batch) captured once at padded shapes:
