@@ -121,7 +121,11 @@ def build_graph(edge_index: torch.Tensor, num_nodes: int, transpose: bool = True
     index_select / scatter bounds checks).  That read is the build's only
     host sync for graphs below HUB_MIN_EDGES; larger graphs read their
     maximum degrees in the same sync (and a skewed one a second time, for
-    the hub plan's size).
+    the hub plan's size).  While the current stream is capturing a HIP graph
+    nothing can be read back: the build (up to CAPTURE_MAX_EDGES edges) is
+    recorded with the range flag left on the device (``SageGraph.bad``,
+    ``SageGraph.check()``).  An edge whose two ends both equal ``num_nodes``
+    is padding and is ignored (fixed-shape edge_index buffers).
     """
     E = int(edge_index.size(1))
     if edge_index.device.type == "cpu":
